@@ -1,0 +1,120 @@
+"""Loader for libcadence_hip.so, the C ABI of include/cadence_kernels.h.
+
+The library is built in-tree (`make -C cadence-gemma_amd`) and loaded with
+ctypes after torch, so it binds to the HIP runtime torch already mapped (one
+runtime per process; verified by `hip_runtimes_loaded`).  There is no CPU
+fallback: if the library is missing, every op raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (load torch's HIP runtime first)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
+ABI_VERSION = 1
+
+_lock = threading.Lock()
+_lib: ctypes.CDLL | None = None
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int
+F32 = ctypes.c_float
+
+# name -> argtypes (restype int unless listed in _RESTYPE)
+_SIGS: dict[str, list] = {
+    "cadence_abi_version": [],
+    "cadence_gemm_workspace_bytes": [I64, I64, I64, I64],
+    "cadence_gemm_linear": [P, I64, P, I64, P, P, I64, P, I64, I64, I64, I64,
+                            I32, I64, I64, I64, P, I64, P],
+    "cadence_gemm_gated_gelu": [P, I64, P, P, P, P, I64, I64, I64, I64, P, I64,
+                                P],
+    "cadence_rglru_gates": [P, I64, P, P, P, P, P, P, P, I64, I64, I64, I64, P,
+                            I64, P],
+    "cadence_gemm_vit_residual": [P, I64, P, I64, P, P, P, I64, I64, I64, I64,
+                                  P, I64, P],
+    "cadence_gemm_patch_embed": [P, I64, P, I64, P, P, P, I64, I64, I64, I64,
+                                 I64, I64, P, I64, P],
+    "cadence_logits_argmax": [P, I64, P, I64, I64, I64, F32, P, P, P, I64, P],
+    "cadence_logits_scratch_bytes": [I64, I64, I64],
+    "cadence_gemm_logits": [P, I64, P, I64, I64, I64, F32, P, I64, P, I64, P],
+    "cadence_rmsnorm": [P, I64, P, P, I64, I64, I64, F32, P],
+    "cadence_layernorm": [P, I64, P, P, P, I64, I64, I64, F32, P],
+    "cadence_embed": [P, P, P, I64, I64, I64, F32, I64, I64, I64, P],
+    "cadence_conv1d": [P, I64, P, P, P, P, P, I64, P, I64, I64, I64, I64, I32,
+                       P],
+    "cadence_rnn_scan": [P, I64, P, I64, P, P, P, I64, P, I64, P, I64, I64, I64,
+                         P],
+    "cadence_segment_info": [P, P, P, I64, I64, P],
+    "cadence_rope_qkv": [P, I64, P, P, P, P, I64, I64, I64, P],
+    "cadence_local_attention": [P, P, P, P, P, P, I64, I64, I64, I64, I64, P],
+    "cadence_kv_cache_fill": [P, P, P, P, P, P, I64, I64, I64, I64, P],
+    "cadence_local_attention_decode": [P, P, P, P, P, P, P, I64, I64, I64, I64,
+                                       P],
+    "cadence_im2col_normalize": [P, P, I64, I64, I64, I64, P, P, P],
+    "cadence_vit_prefix": [P, P, I64, I64, I64, I64, P],
+    "cadence_vit_attention": [P, P, I64, I64, I64, I64, P],
+    "cadence_vit_features": [P, P, I64, I64, I64, I64, I64, I64, P],
+    "cadence_splice_positions": [P, P, I64, I64, I64, P],
+    "cadence_decode_advance": [P, P, I64, P, P, I64, P],
+}
+_RESTYPE = {
+    "cadence_gemm_workspace_bytes": I64,
+    "cadence_logits_scratch_bytes": I64,
+}
+
+
+class KernelLibraryMissing(RuntimeError):
+  pass
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+  for name, args in _SIGS.items():
+    fn = getattr(lib, name)
+    fn.argtypes = args
+    fn.restype = _RESTYPE.get(name, I32)
+
+
+def load() -> ctypes.CDLL:
+  """Returns the loaded kernel library; raises if it is not built."""
+  global _lib
+  if _lib is not None:
+    return _lib
+  with _lock:
+    if _lib is None:
+      if not os.path.exists(LIB_PATH):
+        raise KernelLibraryMissing(
+            f"{LIB_PATH} is missing: build it with `make -C "
+            f"{os.path.dirname(_HERE)}` (hipcc --offload-arch=gfx950). The "
+            "MI355X path has no CPU fallback.")
+      lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+      _declare(lib)
+      v = lib.cadence_abi_version()
+      if v != ABI_VERSION:
+        raise KernelLibraryMissing(f"ABI mismatch: library {v}, host {ABI_VERSION}")
+      _lib = lib
+  return _lib
+
+
+def exported_symbols() -> list[str]:
+  return sorted(_SIGS)
+
+
+def hip_runtimes_loaded() -> list[str]:
+  """Paths of every libamdhip64 mapped into this process."""
+  found = set()
+  with open("/proc/self/maps") as f:
+    for line in f:
+      if "libamdhip64" in line:
+        found.add(line.split()[-1])
+  return sorted(found)
+
+
+def check(status: int, what: str) -> None:
+  if status != 0:
+    raise RuntimeError(f"{what} failed with hipError {status}")

@@ -1,0 +1,378 @@
+"""Griffin blocks on MI355X.
+
+Public surface of the reference `recurrentgemma/torch/modules.py`: the cache
+NamedTuples (:33-50), `LocalAttentionBlock` (:298-500), `RecurrentBlock`
+(:503-685), `MLPBlock` (:688-757), `ResidualBlock` (:759-946) and `Embedder`
+(:949-1006), with the same parameter names, initialisers, forward
+signatures and cache-ownership rules (decode-mode attention caches are
+updated in place and returned, modules.py:210-218).
+
+Each block runs as a short chain of fused gfx950 kernels:
+  recurrent:  rmsnorm -> [linear_y | linear_x] GEMM -> conv1d ->
+              BDL-gates GEMM (gate chain fused) -> scan (x * y fused) ->
+              linear_out GEMM (+bias +residual)
+  attention:  rmsnorm -> [q | k | v] GEMM -> RoPE -> flash MQA ->
+              proj_final GEMM (+bias +residual)
+  MLP:        rmsnorm -> up GEMM (gelu_tanh(gate) * up fused) ->
+              ffw_down GEMM (+bias +residual)
+"""
+
+from __future__ import annotations
+
+import math
+from typing import NamedTuple
+
+import torch
+from torch import nn
+
+from . import common, layers, ops
+from .layers import PackCache, _flat, positions_2d
+
+
+class RecurrentBlockCache(NamedTuple):
+  rg_lru_state: torch.Tensor      # [B, E] fp32
+  conv1d_state: torch.Tensor      # [B, W-1, E]
+
+
+class AttentionBlockCache(NamedTuple):
+  keys: torch.Tensor              # [B, window, 1, head_dim]
+  values: torch.Tensor            # [B, window, 1, head_dim]
+  num_tokens: torch.Tensor        # [B] int32
+
+
+ResidualBlockCache = RecurrentBlockCache | AttentionBlockCache
+
+
+def gelu(x: torch.Tensor) -> torch.Tensor:
+  """tanh-approximated GELU (reference modules.py:293-295)."""
+  return nn.functional.gelu(x, approximate="tanh")
+
+
+class LocalAttentionBlock(nn.Module):
+  """Local multi-query attention (one shared key/value head)."""
+
+  def __init__(self, width: int, num_heads: int, window_size: int,
+               final_w_init_variance_scale: float = 1.0, device=None,
+               dtype=None):
+    super().__init__()
+    self.width = width
+    self.num_heads = num_heads
+    self.window_size = window_size
+    self.final_w_init_variance_scale = final_w_init_variance_scale
+    kw = dict(device=device, dtype=dtype)
+    self.proj_q = nn.Linear(width, width, bias=False, **kw)
+    self.proj_k = nn.Linear(width, self.head_dim, bias=False, **kw)
+    self.proj_v = nn.Linear(width, self.head_dim, bias=False, **kw)
+    self.proj_final = nn.Linear(width, width, bias=True, **kw)
+    self._packed = PackCache()
+    self.reset_parameters()
+
+  @property
+  def head_dim(self) -> int:
+    return self.width // self.num_heads
+
+  def reset_parameters(self) -> None:
+    for lin in (self.proj_q, self.proj_k, self.proj_v):
+      self.w_init_(lin.weight)
+    self.out_w_init_(self.proj_final.weight)
+    nn.init.zeros_(self.proj_final.bias)
+
+  def w_init_(self, w):
+    nn.init.normal_(w, mean=0.0, std=math.sqrt(1.0 / self.width))
+
+  def out_w_init_(self, w):
+    nn.init.normal_(w, mean=0.0, std=math.sqrt(
+        self.final_w_init_variance_scale / self.width))
+
+  def qkv_weight(self):
+    return self._packed.get(
+        [self.proj_q.weight, self.proj_k.weight, self.proj_v.weight],
+        lambda: torch.cat([self.proj_q.weight, self.proj_k.weight,
+                           self.proj_v.weight]).contiguous())
+
+  def fused(self, xn2d, pos, b, t, cache, return_cache, resid2d):
+    """Attention branch on normalised rows; returns (resid + out, cache)."""
+    h, hd = self.num_heads, self.head_dim
+    qkv = ops.linear(xn2d, self.qkv_weight())
+    q, k, v = ops.ops.rope_qkv(qkv, pos.view(-1), h, hd)
+    if cache is None:
+      seg, start = ops.ops.segment_info(pos)
+      enc = ops.ops.local_attention(q, k, v, seg, start, b, t, h, hd,
+                                    self.window_size)
+      new_cache = None
+      if return_cache:
+        ck, cv, nt = ops.ops.kv_cache_fill(k, v, pos, self.window_size)
+        new_cache = AttentionBlockCache(ck, cv, nt)
+    else:
+      if t != 1:
+        # reference modules.py:206-225 only supports 1 or >= window tokens
+        raise NotImplementedError()
+      enc = ops.ops.local_attention_decode_(q, k, v, cache.keys, cache.values,
+                                            cache.num_tokens, h)
+      new_cache = cache if return_cache else None
+    out = ops.linear(enc, self.proj_final.weight, self.proj_final.bias,
+                     resid=resid2d)
+    return out, new_cache
+
+  def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,
+              cache: AttentionBlockCache | None = None,
+              return_cache: bool = True):
+    b, t, d = x.shape
+    pos = positions_2d(segment_pos, b, t)
+    zero = torch.zeros(b * t, d, dtype=x.dtype, device=x.device)
+    out, new_cache = self.fused(_flat(x), pos, b, t, cache, return_cache, zero)
+    return out.view(b, t, d), new_cache
+
+  @classmethod
+  def init_cache(cls, batch_size: int, window_size: int, heads_dim: int,
+                 dtype: torch.dtype, device=None) -> AttentionBlockCache:
+    shape = (batch_size, window_size, 1, heads_dim)
+    return AttentionBlockCache(
+        keys=torch.zeros(shape, device=device, dtype=dtype),
+        values=torch.zeros(shape, device=device, dtype=dtype),
+        num_tokens=torch.zeros([batch_size], dtype=torch.int32, device=device))
+
+
+class RecurrentBlock(nn.Module):
+  """Conv1D + RG-LRU branch gated by a linear branch."""
+
+  def __init__(self, width: int, num_heads: int, lru_width: int | None = None,
+               conv1d_temporal_width: int = 4,
+               final_w_init_variance_scale: float = 1.0, device=None,
+               dtype=None, compat: bool = True):
+    super().__init__()
+    self.width = width
+    self.num_heads = num_heads
+    self.lru_width = lru_width or width
+    self.conv1d_temporal_width = conv1d_temporal_width
+    self.final_w_init_variance_scale = final_w_init_variance_scale
+    kw = dict(device=device, dtype=dtype)
+    self.linear_y = nn.Linear(width, self.lru_width, **kw)
+    self.linear_x = nn.Linear(width, self.lru_width, **kw)
+    self.linear_out = nn.Linear(self.lru_width, width, **kw)
+    self.conv_1d = layers.Conv1D(self.lru_width, conv1d_temporal_width,
+                                 compat=compat, **kw)
+    self.rg_lru = layers.RGLRU(self.lru_width, num_heads, **kw)
+    self._packed = PackCache()
+    self.reset_parameters()
+
+  def reset_parameters(self) -> None:
+    self.w_init_(self.linear_x.weight)
+    nn.init.zeros_(self.linear_x.bias)
+    self.w_init_(self.linear_y.weight)
+    nn.init.zeros_(self.linear_y.bias)
+    self.out_w_init_(self.linear_out.weight)
+    nn.init.zeros_(self.linear_out.bias)
+    self.conv_1d.reset_parameters()
+    self.rg_lru.reset_parameters()
+
+  def w_init_(self, w):
+    nn.init.normal_(w, mean=0.0, std=math.sqrt(1.0 / self.width))
+
+  def out_w_init_(self, w):
+    nn.init.normal_(w, mean=0.0, std=math.sqrt(
+        self.final_w_init_variance_scale / self.lru_width))
+
+  def yx_weight(self):
+    src = [self.linear_y.weight, self.linear_x.weight, self.linear_y.bias,
+           self.linear_x.bias]
+    return self._packed.get(src, lambda: (
+        torch.cat([self.linear_y.weight, self.linear_x.weight]).contiguous(),
+        torch.cat([self.linear_y.bias, self.linear_x.bias]).contiguous()))
+
+  def fused(self, xn2d, pos, b, t, cache, return_cache, resid2d,
+            inplace_state: bool = False):
+    e = self.lru_width
+    w, bias = self.yx_weight()
+    yx = ops.linear(xn2d, w, bias)                       # [M, 2E]: y | x
+    y_br, x_br = yx[:, :e], yx[:, e:]
+    conv_out, conv_state = self.conv_1d.apply2d(
+        x_br, pos, None if cache is None else cache.conv1d_state, b, t)
+    a, nx = self.rg_lru.gates(conv_out, pos.view(-1))
+    h0 = None if cache is None else cache.rg_lru_state
+    gated, h_last = ops.ops.rnn_scan(nx, a, None, h0, y_br, b, t)
+    out = ops.linear(gated, self.linear_out.weight, self.linear_out.bias,
+                     resid=resid2d)
+    if not return_cache:
+      return out, None
+    if inplace_state and cache is not None:
+      cache.rg_lru_state.copy_(h_last)
+      cache.conv1d_state.copy_(conv_state)
+      return out, cache
+    return out, RecurrentBlockCache(rg_lru_state=h_last, conv1d_state=conv_state)
+
+  def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,
+              cache: RecurrentBlockCache | None = None,
+              return_cache: bool = True):
+    b, t, d = x.shape
+    pos = positions_2d(segment_pos, b, t)
+    zero = torch.zeros(b * t, d, dtype=x.dtype, device=x.device)
+    out, new_cache = self.fused(_flat(x), pos, b, t, cache, return_cache, zero)
+    return out.view(b, t, d), new_cache
+
+  @classmethod
+  def init_cache(cls, batch_size: int, lru_width: int, dtype: torch.dtype,
+                 conv1d_temporal_width: int = 4,
+                 device=None) -> RecurrentBlockCache:
+    return RecurrentBlockCache(
+        rg_lru_state=layers.RGLRU.init_cache(batch_size, lru_width, device),
+        conv1d_state=layers.Conv1D.init_cache(
+            batch_size=batch_size, width=lru_width, dtype=dtype,
+            conv1d_temporal_width=conv1d_temporal_width, device=device))
+
+
+class MLPBlock(nn.Module):
+  """Gated MLP: ffw_down(gelu_tanh(x W_gate + b) * (x W_up + b))."""
+
+  def __init__(self, width: int, expanded_width: int,
+               final_w_init_variance_scale: float = 1.0, device=None,
+               dtype=None):
+    super().__init__()
+    self.width = width
+    self.expanded_width = expanded_width
+    self.final_w_init_variance_scale = final_w_init_variance_scale
+    kw = dict(device=device, dtype=dtype)
+    self.ffw_up = layers.Einsum((2, width, expanded_width),
+                                (2, 1, 1, expanded_width),
+                                "...td,cdD->c...tD", **kw)
+    self.ffw_down = nn.Linear(expanded_width, width, **kw)
+    self.reset_parameters()
+
+  def reset_parameters(self) -> None:
+    self.ffw_up.reset_parameters()
+    nn.init.normal_(self.ffw_down.weight, mean=0.0, std=math.sqrt(
+        self.final_w_init_variance_scale / self.expanded_width))
+    nn.init.zeros_(self.ffw_down.bias)
+
+  def fused(self, xn2d, resid2d):
+    w, bg, bu = self.ffw_up.gated_packed()
+    act = ops.ops.gated_gelu(xn2d, w, bg, bu)
+    return ops.linear(act, self.ffw_down.weight, self.ffw_down.bias,
+                      resid=resid2d)
+
+  def forward(self, x: torch.Tensor) -> torch.Tensor:
+    zero = torch.zeros(_flat(x).shape, dtype=x.dtype, device=x.device)
+    return self.fused(_flat(x), zero).view(x.shape)
+
+
+class ResidualBlock(nn.Module):
+  """norm -> temporal block -> +res -> norm -> MLP -> +res."""
+
+  def __init__(self, width: int, mlp_expanded_width: int, num_heads: int,
+               attention_window_size: int,
+               temporal_block_type: common.TemporalBlockType,
+               lru_width: int | None = None, conv1d_temporal_width: int = 4,
+               final_w_init_variance_scale: float = 1.0, device=None,
+               dtype=None, compat: bool = True):
+    super().__init__()
+    self.width = width
+    self.mlp_expanded_width = mlp_expanded_width
+    self.num_heads = num_heads
+    self.attention_window_size = attention_window_size
+    self.temporal_block_type = temporal_block_type
+    self.lru_width = lru_width
+    self.conv1d_temporal_width = conv1d_temporal_width
+    self.final_w_init_variance_scale = final_w_init_variance_scale
+    kw = dict(device=device, dtype=dtype)
+    self.temporal_pre_norm = layers.RMSNorm(width, **kw)
+    if temporal_block_type == common.TemporalBlockType.RECURRENT:
+      self.recurrent_block = RecurrentBlock(
+          width, num_heads, lru_width, conv1d_temporal_width,
+          final_w_init_variance_scale, compat=compat, **kw)
+    else:
+      self.attention_block = LocalAttentionBlock(
+          width, num_heads, attention_window_size,
+          final_w_init_variance_scale, **kw)
+    self.channel_pre_norm = layers.RMSNorm(width, **kw)
+    self.mlp_block = MLPBlock(width, mlp_expanded_width,
+                              final_w_init_variance_scale, **kw)
+
+  @property
+  def temporal_block(self) -> nn.Module:
+    if self.temporal_block_type == common.TemporalBlockType.RECURRENT:
+      return self.recurrent_block
+    return self.attention_block
+
+  def reset_parameters(self) -> None:
+    self.temporal_pre_norm.reset_parameters()
+    self.temporal_block.reset_parameters()
+    self.channel_pre_norm.reset_parameters()
+    self.mlp_block.reset_parameters()
+
+  def fused(self, x2d, pos, b, t, cache, return_cache,
+            inplace_state: bool = False):
+    """One residual block on [B*T, D] rows; returns (out rows, cache)."""
+    xn = ops.rmsnorm(x2d, self.temporal_pre_norm.scale,
+                     self.temporal_pre_norm.eps)
+    if self.temporal_block_type == common.TemporalBlockType.RECURRENT:
+      resid, new_cache = self.recurrent_block.fused(
+          xn, pos, b, t, cache, return_cache, x2d, inplace_state)
+    else:
+      resid, new_cache = self.attention_block.fused(
+          xn, pos, b, t, cache, return_cache, x2d)
+    hn = ops.rmsnorm(resid, self.channel_pre_norm.scale,
+                     self.channel_pre_norm.eps)
+    return self.mlp_block.fused(hn, resid), new_cache
+
+  def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,
+              cache: ResidualBlockCache | None = None,
+              return_cache: bool = True):
+    b, t, d = x.shape
+    pos = positions_2d(segment_pos, b, t)
+    out, new_cache = self.fused(_flat(x), pos, b, t, cache, return_cache)
+    return out.view(b, t, d), new_cache
+
+  @classmethod
+  def init_cache(cls, batch_size: int, width: int, num_heads: int,
+                 attention_window_size: int,
+                 temporal_block_type: common.TemporalBlockType,
+                 dtype: torch.dtype, lru_width: int | None = None,
+                 conv1d_temporal_width: int = 4,
+                 device=None) -> ResidualBlockCache:
+    if temporal_block_type == common.TemporalBlockType.RECURRENT:
+      return RecurrentBlock.init_cache(batch_size, lru_width or width, dtype,
+                                       conv1d_temporal_width, device)
+    return LocalAttentionBlock.init_cache(batch_size, attention_window_size,
+                                          width // num_heads, dtype, device)
+
+
+class Embedder(nn.Module):
+  """Token embedding; `decode` is the tied output projection."""
+
+  def __init__(self, vocab_size: int, embed_dim: int, scale_by_sqrt_dim: bool,
+               device=None, dtype=None):
+    super().__init__()
+    self.vocab_size = vocab_size
+    self.embed_dim = embed_dim
+    self.scale_by_sqrt_dim = scale_by_sqrt_dim
+    self.input_embedding = nn.Parameter(torch.empty(
+        [vocab_size, embed_dim], device=device, dtype=dtype))
+    self.reset_parameters()
+
+  def reset_parameters(self) -> None:
+    nn.init.normal_(self.input_embedding, mean=0.0,
+                    std=math.sqrt(1.0 / self.embed_dim))
+
+  @property
+  def scale(self) -> float:
+    # the reference multiplies by a bf16 scalar: bf16(sqrt(2560)) = 50.5
+    if not self.scale_by_sqrt_dim:
+      return 1.0
+    return float(torch.tensor(math.sqrt(self.embed_dim)).to(torch.bfloat16))
+
+  def encode_into(self, tokens: torch.Tensor, out2d: torch.Tensor,
+                  row_map=None):
+    tok = tokens.reshape(-1).to(torch.int32).contiguous()
+    m = tok.numel()
+    div, mul, off = row_map if row_map is not None else (max(m, 1), 0, 0)
+    ops.ops.embed_(tok, self.input_embedding, self.scale, out2d, div, mul, off)
+
+  def encode(self, x: torch.Tensor) -> torch.Tensor:
+    out = torch.empty(x.numel(), self.embed_dim, dtype=self.input_embedding.dtype,
+                      device=x.device)
+    self.encode_into(x, out)
+    return out.view(*x.shape, self.embed_dim)
+
+  def decode(self, x: torch.Tensor) -> torch.Tensor:
+    logits = ops.ops.gemm_logits(_flat(x), self.input_embedding, 0.0)
+    return logits.view(*x.shape[:-1], self.vocab_size)

@@ -1,0 +1,398 @@
+"""torch.ops.cadence.* -- PyTorch-ROCm custom ops over the gfx950 C ABI.
+
+Each op validates dtype / shape / layout (errors surface as RuntimeError,
+like the reference's assert / ValueError sites), allocates its outputs
+through the torch caching allocator, and enqueues the HIP kernels on the
+current stream (graph-capturable: no host sync, no allocation in the C
+layer).  Ops are registered for the CUDA (= HIP on ROCm) dispatch key only;
+there is deliberately no CPU implementation.
+
+Thin Python helpers below the registrations (`linear`, `rmsnorm`, ...) are
+what the modules call; they route through `torch.ops.cadence`.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_BF16 = torch.bfloat16
+_F32 = torch.float32
+_I32 = torch.int32
+
+_LIBDEF = torch.library.Library("cadence", "DEF")
+
+
+def _reg(schema: str):
+  name = schema.split("(")[0]
+  _LIBDEF.define(schema)
+
+  def deco(fn):
+    _LIBDEF.impl(name, fn, "CUDA")
+    return fn
+  return deco
+
+
+def _p(t):
+  return None if t is None else t.data_ptr()
+
+
+def _s(t: torch.Tensor):
+  return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _need(cond: bool, msg: str):
+  if not cond:
+    raise RuntimeError(msg)
+
+
+def _mat(t: torch.Tensor, name: str, dtype=_BF16) -> int:
+  """Validates a row-major 2-D (view) operand and returns its leading dim."""
+  _need(t.dim() == 2, f"{name}: expected 2-D, got {tuple(t.shape)}")
+  _need(t.dtype == dtype, f"{name}: expected {dtype}, got {t.dtype}")
+  _need(t.stride(1) == 1, f"{name}: last dim must be contiguous")
+  return t.stride(0)
+
+
+def _ws(M: int, N: int, K: int, groups: int, like: torch.Tensor):
+  n = _lib.load().cadence_gemm_workspace_bytes(M, N, K, groups)
+  if n == 0:
+    return None, 0
+  return torch.empty(n, dtype=torch.uint8, device=like.device), n
+
+
+# ------------------------------------------------------------------- GEMMs
+
+@_reg("gemm_linear_(Tensor a, Tensor w, Tensor? bias, Tensor? resid, "
+      "Tensor(a!) out, int act, int row_div, int row_mul, int row_off) -> ()")
+def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off):
+  lda, ldw, ldo = _mat(a, "a"), _mat(w, "w"), _mat(out, "out")
+  M, K = a.shape
+  N = w.shape[0]
+  _need(w.shape[1] == K, f"K mismatch {K} vs {w.shape[1]}")
+  ldr = 0
+  if resid is not None:
+    ldr = _mat(resid, "resid")
+  if bias is not None:
+    _need(bias.numel() == N and bias.dtype == _BF16, "bias shape/dtype")
+  ws, nws = _ws(M, N, K, 1, a)
+  _lib.check(_lib.load().cadence_gemm_linear(
+      _p(a), lda, _p(w), ldw, _p(bias), _p(resid), ldr, _p(out), ldo, M, N, K,
+      act, row_div, row_mul, row_off, _p(ws), nws, _s(a)), "gemm_linear")
+
+
+@_reg("gated_gelu(Tensor a, Tensor w_packed, Tensor bias_gate, "
+      "Tensor bias_up) -> Tensor")
+def _gated_gelu(a, w_packed, bias_gate, bias_up):
+  lda = _mat(a, "a")
+  M, K = a.shape
+  F = w_packed.shape[0] // 2
+  _need(w_packed.shape[1] == K and w_packed.is_contiguous(), "w_packed")
+  out = torch.empty(M, F, dtype=_BF16, device=a.device)
+  ws, nws = _ws(M, 2 * F, K, 1, a)
+  _lib.check(_lib.load().cadence_gemm_gated_gelu(
+      _p(a), lda, _p(w_packed), _p(bias_gate), _p(bias_up), _p(out), F, M, F,
+      K, _p(ws), nws, _s(a)), "gated_gelu")
+  return out
+
+
+@_reg("rglru_gates(Tensor x, Tensor w_packed, Tensor bias_x, Tensor bias_a, "
+      "Tensor softplus_a, Tensor segment_pos) -> (Tensor, Tensor)")
+def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos):
+  ldx = _mat(x, "x")
+  M, E = x.shape
+  H, two_bw, bw = w_packed.shape
+  _need(two_bw == 2 * bw and H * bw == E, "w_packed shape")
+  _need(segment_pos.dtype == _I32 and segment_pos.numel() == M, "segment_pos")
+  a = torch.empty(M, E, dtype=_BF16, device=x.device)
+  nx = torch.empty(M, E, dtype=_BF16, device=x.device)
+  ws, nws = _ws(M, 2 * bw, bw, H, x)
+  _lib.check(_lib.load().cadence_rglru_gates(
+      _p(x), ldx, _p(w_packed), _p(bias_x), _p(bias_a), _p(softplus_a),
+      _p(segment_pos.contiguous()), _p(a), _p(nx), E, M, H, bw, _p(ws), nws,
+      _s(x)), "rglru_gates")
+  return a, nx
+
+
+@_reg("vit_residual_(Tensor a, Tensor w, Tensor bias, Tensor? gamma, "
+      "Tensor(a!) resid) -> ()")
+def _vit_residual(a, w, bias, gamma, resid):
+  lda, ldw = _mat(a, "a"), _mat(w, "w")
+  ldr = _mat(resid, "resid", _F32)
+  M, K = a.shape
+  N = w.shape[0]
+  ws, nws = _ws(M, N, K, 1, a)
+  _lib.check(_lib.load().cadence_gemm_vit_residual(
+      _p(a), lda, _p(w), ldw, _p(bias), _p(gamma), _p(resid), ldr, M, N, K,
+      _p(ws), nws, _s(a)), "vit_residual")
+
+
+@_reg("patch_embed_(Tensor patches, Tensor w, Tensor bias, Tensor pos, "
+      "Tensor(a!) resid, int B, int P, int ntok, int prefix) -> ()")
+def _patch_embed(patches, w, bias, pos, resid, B, P, ntok, prefix):
+  ldp, ldw = _mat(patches, "patches"), _mat(w, "w")
+  N, K = w.shape
+  _need(resid.dtype == _F32 and resid.is_contiguous(), "resid")
+  ws, nws = _ws(B * P, N, K, 1, patches)
+  _lib.check(_lib.load().cadence_gemm_patch_embed(
+      _p(patches), ldp, _p(w), ldw, _p(bias), _p(pos), _p(resid), B, P, ntok,
+      prefix, N, K, _p(ws), nws, _s(patches)), "patch_embed")
+
+
+@_reg("logits_argmax(Tensor x, Tensor embedding, float soft_cap, "
+      "bool return_logits) -> (Tensor, Tensor)")
+def _logits_argmax(x, embedding, soft_cap, return_logits):
+  ldx = _mat(x, "x")
+  M, D = x.shape
+  V = embedding.shape[0]
+  L = _lib.load()
+  nscr = L.cadence_logits_scratch_bytes(M, V, D)
+  scratch = torch.empty(nscr, dtype=torch.uint8, device=x.device)
+  logits = torch.empty((M, V) if return_logits else (0,), dtype=_BF16,
+                       device=x.device)
+  nxt = torch.empty(M, dtype=_I32, device=x.device)
+  _lib.check(L.cadence_logits_argmax(
+      _p(x), ldx, _p(embedding), M, V, D, float(soft_cap),
+      _p(logits) if return_logits else None, _p(nxt), _p(scratch), nscr,
+      _s(x)), "logits_argmax")
+  return logits, nxt
+
+
+@_reg("gemm_logits(Tensor x, Tensor embedding, float soft_cap) -> Tensor")
+def _gemm_logits(x, embedding, soft_cap):
+  ldx = _mat(x, "x")
+  M, D = x.shape
+  V = embedding.shape[0]
+  out = torch.empty(M, V, dtype=_BF16, device=x.device)
+  ws, nws = _ws(M, V, D, 1, x)
+  _lib.check(_lib.load().cadence_gemm_logits(
+      _p(x), ldx, _p(embedding), M, V, D, float(soft_cap), _p(out), V, _p(ws),
+      nws, _s(x)), "gemm_logits")
+  return out
+
+
+# ------------------------------------------------------ norms / embedding
+
+@_reg("rmsnorm(Tensor x, Tensor scale, float eps) -> Tensor")
+def _rmsnorm(x, scale, eps):
+  ldx = _mat(x, "x")
+  out = torch.empty(x.shape, dtype=_BF16, device=x.device)
+  _lib.check(_lib.load().cadence_rmsnorm(
+      _p(x), ldx, _p(scale), _p(out), x.shape[1], x.shape[0], x.shape[1],
+      float(eps), _s(x)), "rmsnorm")
+  return out
+
+
+@_reg("layernorm(Tensor x, Tensor weight, Tensor bias, float eps) -> Tensor")
+def _layernorm(x, weight, bias, eps):
+  ldx = _mat(x, "x", _F32)
+  out = torch.empty(x.shape, dtype=_BF16, device=x.device)
+  _lib.check(_lib.load().cadence_layernorm(
+      _p(x), ldx, _p(weight), _p(bias), _p(out), x.shape[1], x.shape[0],
+      x.shape[1], float(eps), _s(x)), "layernorm")
+  return out
+
+
+@_reg("embed_(Tensor tokens, Tensor embedding, float scale, Tensor(a!) out, "
+      "int row_div, int row_mul, int row_off) -> ()")
+def _embed(tokens, embedding, scale, out, row_div, row_mul, row_off):
+  _need(tokens.dtype == _I32 and tokens.is_contiguous(), "tokens int32")
+  ldo = _mat(out, "out")
+  _lib.check(_lib.load().cadence_embed(
+      _p(tokens), _p(embedding), _p(out), ldo, tokens.numel(),
+      embedding.shape[1], float(scale), row_div, row_mul, row_off,
+      _s(tokens)), "embed")
+
+
+# -------------------------------------------------------- recurrent block
+
+@_reg("conv1d(Tensor x, Tensor w, Tensor b, Tensor segment_pos, Tensor? cache, "
+      "int B, int L, bool compat) -> (Tensor, Tensor)")
+def _conv1d(x, w, b, segment_pos, cache, B, L, compat):
+  ldx = _mat(x, "x")
+  E = x.shape[1]
+  TW = w.shape[0]
+  out = torch.empty(B * L, E, dtype=_BF16, device=x.device)
+  new_cache = torch.empty(B, TW - 1, E, dtype=_BF16, device=x.device)
+  if cache is not None:
+    _need(L == 1 and tuple(cache.shape) == (B, TW - 1, E), "conv cache shape")
+    cache = cache.to(_BF16).contiguous()
+  _lib.check(_lib.load().cadence_conv1d(
+      _p(x), ldx, _p(w), _p(b), _p(segment_pos.contiguous()), _p(cache),
+      _p(out), E, _p(new_cache), B, L, E, TW, int(compat), _s(x)), "conv1d")
+  return out, new_cache
+
+
+@_reg("rnn_scan(Tensor x, Tensor a, Tensor? segment_pos, Tensor? h0, "
+      "Tensor? gate, int B, int L) -> (Tensor, Tensor)")
+def _rnn_scan(x, a, segment_pos, h0, gate, B, L):
+  ldx, lda = _mat(x, "x"), _mat(a, "a")
+  E = x.shape[1]
+  ldg = _mat(gate, "gate") if gate is not None else 0
+  if h0 is not None:
+    _need(h0.dtype == _F32 and h0.is_contiguous(), "h0 fp32")
+  out = torch.empty(B * L, E, dtype=_BF16, device=x.device)
+  h_last = torch.empty(B, E, dtype=_F32, device=x.device)
+  pos = segment_pos.contiguous() if segment_pos is not None else None
+  _lib.check(_lib.load().cadence_rnn_scan(
+      _p(x), ldx, _p(a), lda, _p(pos), _p(h0), _p(gate), ldg, _p(out), E,
+      _p(h_last), B, L, E, _s(x)), "rnn_scan")
+  return out, h_last
+
+
+# ---------------------------------------------------------------- attention
+
+@_reg("segment_info(Tensor segment_pos) -> (Tensor, Tensor)")
+def _segment_info(segment_pos):
+  B, L = segment_pos.shape
+  seg = torch.empty(B, L, dtype=_I32, device=segment_pos.device)
+  start = torch.empty(B, L, dtype=_I32, device=segment_pos.device)
+  _lib.check(_lib.load().cadence_segment_info(
+      _p(segment_pos.contiguous()), _p(seg), _p(start), B, L,
+      _s(segment_pos)), "segment_info")
+  return seg, start
+
+
+@_reg("rope_qkv(Tensor qkv, Tensor positions, int H, int hd) -> "
+      "(Tensor, Tensor, Tensor)")
+def _rope_qkv(qkv, positions, H, hd):
+  ld = _mat(qkv, "qkv")
+  M = qkv.shape[0]
+  q = torch.empty(M, H * hd, dtype=_BF16, device=qkv.device)
+  k = torch.empty(M, hd, dtype=_BF16, device=qkv.device)
+  v = torch.empty(M, hd, dtype=_BF16, device=qkv.device)
+  _lib.check(_lib.load().cadence_rope_qkv(
+      _p(qkv), ld, _p(positions.contiguous()), _p(q), _p(k), _p(v), M, H, hd,
+      _s(qkv)), "rope_qkv")
+  return q, k, v
+
+
+@_reg("local_attention(Tensor q, Tensor k, Tensor v, Tensor seg_id, "
+      "Tensor seg_start, int B, int L, int H, int hd, int window) -> Tensor")
+def _local_attention(q, k, v, seg_id, seg_start, B, L, H, hd, window):
+  for t in (q, k, v):
+    _need(t.is_contiguous() and t.dtype == _BF16, "q/k/v contiguous bf16")
+  out = torch.empty(B * L, H * hd, dtype=_BF16, device=q.device)
+  _lib.check(_lib.load().cadence_local_attention(
+      _p(q), _p(k), _p(v), _p(seg_id), _p(seg_start), _p(out), B, L, H, hd,
+      window, _s(q)), "local_attention")
+  return out
+
+
+@_reg("kv_cache_fill(Tensor k, Tensor v, Tensor segment_pos, int window) -> "
+      "(Tensor, Tensor, Tensor)")
+def _kv_cache_fill(k, v, segment_pos, window):
+  B, L = segment_pos.shape
+  hd = k.shape[-1]
+  ck = torch.empty(B, window, 1, hd, dtype=_BF16, device=k.device)
+  cv = torch.empty(B, window, 1, hd, dtype=_BF16, device=k.device)
+  nt = torch.empty(B, dtype=_I32, device=k.device)
+  _lib.check(_lib.load().cadence_kv_cache_fill(
+      _p(k), _p(v), _p(segment_pos.contiguous()), _p(ck), _p(cv), _p(nt), B,
+      L, hd, window, _s(k)), "kv_cache_fill")
+  return ck, cv, nt
+
+
+@_reg("local_attention_decode_(Tensor q, Tensor k_new, Tensor v_new, "
+      "Tensor(a!) cache_k, Tensor(b!) cache_v, Tensor(c!) num_tokens, int H) "
+      "-> Tensor")
+def _local_attention_decode(q, k_new, v_new, cache_k, cache_v, num_tokens, H):
+  B = q.shape[0]
+  hd = k_new.shape[-1]
+  W = cache_k.shape[1]
+  _need(cache_k.is_contiguous() and cache_v.is_contiguous(), "cache layout")
+  _need(num_tokens.dtype == _I32, "num_tokens int32")
+  out = torch.empty(B, H * hd, dtype=_BF16, device=q.device)
+  _lib.check(_lib.load().cadence_local_attention_decode(
+      _p(q.contiguous()), _p(k_new.contiguous()), _p(v_new.contiguous()),
+      _p(cache_k), _p(cache_v), _p(num_tokens), _p(out), B, H, hd, W, _s(q)),
+      "local_attention_decode")
+  return out
+
+
+# ------------------------------------------------------------- vision tower
+
+@_reg("im2col_normalize(Tensor pixels, float[] mean, float[] std, int patch, "
+      "int kpad) -> Tensor")
+def _im2col(pixels, mean, std, patch, kpad):
+  import ctypes
+  _need(pixels.dtype == _F32 and pixels.is_contiguous(), "pixels fp32")
+  B, C, S, S2 = pixels.shape
+  _need(C == 3 and S == S2 and len(mean) == 3 and len(std) == 3,
+        "pixels [B,3,S,S], 3 means / stds")
+  g = S // patch
+  out = torch.empty(B * g * g, kpad, dtype=_BF16, device=pixels.device)
+  m3 = (ctypes.c_float * 3)(*[float(v) for v in mean])
+  s3 = (ctypes.c_float * 3)(*[float(v) for v in std])
+  _lib.check(_lib.load().cadence_im2col_normalize(
+      _p(pixels), _p(out), kpad, B, S, patch, ctypes.cast(m3, ctypes.c_void_p),
+      ctypes.cast(s3, ctypes.c_void_p), _s(pixels)), "im2col")
+  return out
+
+
+@_reg("vit_prefix_(Tensor tokens, Tensor(a!) resid, int B, int ntok, "
+      "int prefix) -> ()")
+def _vit_prefix(tokens, resid, B, ntok, prefix):
+  _lib.check(_lib.load().cadence_vit_prefix(
+      _p(tokens.contiguous()), _p(resid), B, ntok, prefix, resid.shape[-1],
+      _s(resid)), "vit_prefix")
+
+
+@_reg("vit_attention(Tensor qkv, int B, int N, int H, int hd) -> Tensor")
+def _vit_attention(qkv, B, N, H, hd):
+  _need(qkv.is_contiguous() and qkv.dtype == _BF16, "qkv contiguous bf16")
+  out = torch.empty(B * N, H * hd, dtype=_BF16, device=qkv.device)
+  _lib.check(_lib.load().cadence_vit_attention(
+      _p(qkv), _p(out), B, N, H, hd, _s(qkv)), "vit_attention")
+  return out
+
+
+@_reg("vit_features_(Tensor resid, Tensor(a!) out, int col_off, int B, "
+      "int ntok, int prefix) -> ()")
+def _vit_features(resid, out, col_off, B, ntok, prefix):
+  ldo = _mat(out, "out")
+  _lib.check(_lib.load().cadence_vit_features(
+      _p(resid), _p(out), ldo, col_off, B, ntok, prefix, resid.shape[-1],
+      _s(resid)), "vit_features")
+
+
+@_reg("splice_positions(Tensor text_pos, int n_vis) -> Tensor")
+def _splice_positions(text_pos, n_vis):
+  B, T = text_pos.shape
+  out = torch.empty(B, n_vis + T, dtype=_I32, device=text_pos.device)
+  _lib.check(_lib.load().cadence_splice_positions(
+      _p(text_pos.contiguous()), _p(out), B, T, n_vis, _s(text_pos)),
+      "splice_positions")
+  return out
+
+
+@_reg("decode_advance_(Tensor next_token, Tensor(a!) tokens_out, "
+      "Tensor(b!) step, Tensor(c!) positions) -> ()")
+def _decode_advance(next_token, tokens_out, step, positions):
+  B = next_token.numel()
+  _need(tokens_out.dtype == _I32 and tokens_out.stride(1) == 1, "tokens_out")
+  _lib.check(_lib.load().cadence_decode_advance(
+      _p(next_token), _p(tokens_out), tokens_out.stride(0), _p(step),
+      _p(positions), B, _s(next_token)), "decode_advance")
+
+
+# ----------------------------------------------------------------- helpers
+
+ops = torch.ops.cadence
+
+
+def linear(x2d, w, bias=None, act=0, resid=None, out=None,
+           row_map=None):
+  """out = act(x2d . w^T + bias) (+ resid); w [N, K] (nn.Linear layout)."""
+  M = x2d.shape[0]
+  N = w.shape[0]
+  if out is None:
+    out = torch.empty(M, N, dtype=_BF16, device=x2d.device)
+  div, mul, off = row_map if row_map is not None else (max(M, 1), 0, 0)
+  ops.gemm_linear_(x2d, w, bias, resid, out, act, div, mul, off)
+  return out
+
+
+def rmsnorm(x2d, scale, eps=1e-6):
+  return ops.rmsnorm(x2d, scale, eps)

@@ -1,0 +1,235 @@
+"""Greedy / categorical sampler for the MI355X Griffin.
+
+Keeps the API of the reference `recurrentgemma/torch/sampler.py`
+(`SamplingState` :33-53, `SamplerOutput` :56-67, `Sampler(model, vocab,
+greedy_sampling, is_it_model)` :70-109, `__call__(input_strings,
+total_generation_steps, echo, return_logits, end_sampling_at_eos_token,
+img_path)` :377-449) with the position semantics of the working multimodal
+sampler `examples/cadence_sampler.py` (:185-298): left-padded prompts,
+positions `arange(T) - T + len` clipped at -1, prefill on tokens[:, :-1]
+(image spliced there), one cached step on the last prompt token, then
+single-token decode.  The library's `prompt_length += 729` /
+`input_lengths + 1` bugs are not reproduced.
+
+Decode runs on device: soft-cap + argmax are fused into the logits kernel,
+the next token / positions / step counter are advanced by a kernel, and the
+whole step can be captured once into a hipGraph and replayed
+(`use_graph=True`), so the loop has no per-step host sync.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from typing import Generic, NamedTuple, Sequence, TypeVar
+
+import torch
+
+from . import common, ops
+
+Cache = TypeVar("Cache")
+
+
+@dataclasses.dataclass
+class SamplingState(Generic[Cache]):
+  tokens_buffer: torch.Tensor
+  step: torch.Tensor
+  total_steps: torch.Tensor
+  positions: torch.Tensor
+  cache: Cache
+  done: torch.Tensor
+  logits_buffer: torch.Tensor | None = None
+
+
+class SamplerOutput(NamedTuple):
+  text: list[str]
+  logits: list[torch.Tensor]
+  tokens: list[torch.Tensor]
+
+
+def prompt_positions(lengths: torch.Tensor, prompt_length: int) -> torch.Tensor:
+  """examples/cadence_sampler.py:198-201."""
+  pos = torch.arange(prompt_length, dtype=torch.int32)[None].repeat(
+      lengths.shape[0], 1)
+  pos = pos - prompt_length + lengths.to(torch.int32)[:, None]
+  return torch.clip(pos, min=-1)
+
+
+class Sampler:
+  """Sampler for a `cadence.Griffin` model."""
+
+  def __init__(self, model, vocab, greedy_sampling: bool = True,
+               is_it_model: bool = False, use_graph: bool = True):
+    self.model = model
+    self.vocab = vocab
+    self.greedy_sampling = greedy_sampling
+    self._is_it_model = is_it_model
+    self.use_graph = use_graph
+    self._eos_token = torch.tensor([self.vocab.eos_id()], device=self.device)
+
+  @property
+  def dtype(self) -> torch.dtype:
+    return next(self.model.parameters()).dtype
+
+  @property
+  def device(self) -> torch.device:
+    return next(self.model.parameters()).device
+
+  @property
+  def vocab_size(self) -> int:
+    return self.model.config.vocab_size
+
+  def apply_model(self, tokens, segment_pos, cache=None, return_logits=True,
+                  return_cache=True, img_path=None, images=None):
+    return self.model(tokens=tokens, segment_pos=segment_pos, cache=cache,
+                      return_logits=return_logits, return_cache=return_cache,
+                      img_path=img_path, images=images)
+
+  def tokenize(self, input_string: str) -> torch.Tensor:
+    if self._is_it_model:
+      input_string = common.apply_it_formatter(input_string)
+    ids = [self.vocab.bos_id()] + list(self.vocab.EncodeAsIds(input_string))
+    return torch.tensor(ids, dtype=torch.int32)
+
+  def _get_padded_tokens(self, tokens: Sequence[torch.Tensor]) -> torch.Tensor:
+    n = max(len(t) for t in tokens)
+    rows = [torch.cat([torch.full([n - len(t)], self.vocab.pad_id(),
+                                  dtype=torch.int32), t]) for t in tokens]
+    return torch.stack(rows)
+
+  # ------------------------------------------------------------ generation
+
+  @torch.no_grad()
+  def generate(self, tokens: torch.Tensor, input_lengths: torch.Tensor,
+               total_generation_steps: int, images=None, img_path=None,
+               return_logits: bool = False, echo: bool = False,
+               end_sampling_at_eos_token: bool = False) -> SamplingState:
+    """Prefill + decode for a left-padded [B, T] prompt batch (on device)."""
+    dev = self.device
+    b, t = tokens.shape
+    positions = prompt_positions(input_lengths.cpu(), t).to(dev)
+    tokens = tokens.to(dev, torch.int32)
+    steps = total_generation_steps
+    if steps == 0:
+      prev_logits, _ = self.apply_model(tokens, positions, None,
+                                        return_logits and echo, False,
+                                        img_path, images)
+      buf = tokens if echo else torch.empty(b, 0, dtype=torch.int32, device=dev)
+      lb = prev_logits[:, -t:] if (return_logits and echo) else None
+      return SamplingState(buf, torch.tensor(0), torch.tensor(0), positions,
+                           None, torch.zeros(b, dtype=torch.bool), lb)
+    model = self.model
+    prev_logits = None
+    if t > 1:
+      prev_logits, cache = self.apply_model(tokens[:, :-1], positions[:, :-1],
+                                            None, return_logits and echo, True,
+                                            img_path, images)
+      nxt, logits, cache = model.next_token(tokens[:, -1:], positions[:, -1:],
+                                            cache, return_logits)
+    else:
+      logits_all, cache = self.apply_model(tokens, positions, None, True, True,
+                                           img_path, images)
+      logits = logits_all[:, -1]
+      nxt = self._sample(logits)
+    if not self.greedy_sampling:
+      nxt = self._sample(logits)
+    first_logits = logits
+    buf = torch.full((b, steps), self.vocab.pad_id(), dtype=torch.int32,
+                     device=dev)
+    buf[:, 0] = nxt
+    lbuf = None
+    if return_logits:
+      lbuf = torch.zeros(b, steps, self.vocab_size, dtype=self.dtype,
+                         device=dev)
+      lbuf[:, 0] = logits
+    pos = (positions[:, -1] + 1).contiguous()
+    step = torch.ones(1, dtype=torch.int32, device=dev)
+    cur = nxt.to(torch.int32).contiguous()
+    n_more = steps - 1
+    graphable = (self.use_graph and self.greedy_sampling and not return_logits
+                 and n_more > 1)
+    if graphable:
+      self._decode_graph(cur, pos, cache, buf, step, n_more,
+                         end_sampling_at_eos_token)
+    else:
+      for i in range(n_more):
+        nxt, logits, cache = model.next_token(cur[:, None], pos[:, None], cache,
+                                              return_logits or not
+                                              self.greedy_sampling)
+        if not self.greedy_sampling:
+          nxt = self._sample(logits)
+        if return_logits:
+          lbuf[:, i + 1] = logits
+        ops.ops.decode_advance_(nxt, buf, step, pos)
+        cur.copy_(nxt)
+        if end_sampling_at_eos_token and (i % 8 == 7) and self._all_done(buf):
+          break
+    if echo:
+      buf = torch.cat([tokens, buf], dim=1)
+      if return_logits:
+        # examples/cadence_sampler.py:283: [prev_logits, logits, buffer] -- the
+        # last prompt position's logits appear twice (also buffer[:, 0]).
+        prompt_logits = prev_logits[:, -(t - 1):] if t > 1 else lbuf[:, :0]
+        lbuf = torch.cat([prompt_logits, first_logits[:, None].to(lbuf.dtype),
+                          lbuf], dim=1)
+    return SamplingState(buf, step, torch.tensor(steps), pos[:, None], cache,
+                         torch.zeros(b, dtype=torch.bool), lbuf)
+
+  def _sample(self, logits: torch.Tensor) -> torch.Tensor:
+    if self.greedy_sampling:
+      return torch.argmax(logits, dim=-1).to(torch.int32)
+    return torch.distributions.Categorical(logits=logits.float()).sample().to(
+        torch.int32)
+
+  def _all_done(self, buf: torch.Tensor) -> bool:
+    return bool((buf == self.vocab.eos_id()).any(dim=1).all())
+
+  def _decode_graph(self, cur, pos, cache, buf, step, n_more, eos_stop):
+    """Captures one in-place decode step into a hipGraph and replays it."""
+    model = self.model
+    stream = torch.cuda.Stream(device=cur.device)
+    stream.wait_stream(torch.cuda.current_stream(cur.device))
+
+    def one_step():
+      nxt, _, _ = model.next_token(cur[:, None], pos[:, None], cache, False,
+                                   inplace=True)
+      ops.ops.decode_advance_(nxt, buf, step, pos)
+      cur.copy_(nxt)
+
+    with torch.cuda.stream(stream):
+      one_step()                      # step 1 eagerly (also warms the pools)
+      graph = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(graph, stream=stream):
+        one_step()
+      # the capture recorded but did not execute step 2: replay covers it
+      for i in range(n_more - 1):
+        graph.replay()
+        if eos_stop and (i % 8 == 7) and self._all_done(buf):
+          break
+    torch.cuda.current_stream(cur.device).wait_stream(stream)
+
+  # ------------------------------------------------------------------- API
+
+  @torch.no_grad()
+  def __call__(self, input_strings: Sequence[str], total_generation_steps: int,
+               echo: bool = False, return_logits: bool = False,
+               end_sampling_at_eos_token: bool = True,
+               img_path: str | None = None,
+               images: torch.Tensor | None = None) -> SamplerOutput:
+    if total_generation_steps < 0:
+      raise ValueError("total_generation_steps must be at least 0.")
+    ids = [self.tokenize(s) for s in input_strings]
+    lengths = torch.tensor([len(x) for x in ids], dtype=torch.int32)
+    padded = self._get_padded_tokens(ids)
+    pad_lengths = padded.shape[1] - lengths
+    state = self.generate(padded, lengths, total_generation_steps, images,
+                          img_path, return_logits, echo,
+                          end_sampling_at_eos_token)
+    toks = [row[int(l):].cpu() for row, l in zip(state.tokens_buffer,
+                                                  pad_lengths)]
+    logits = []
+    if return_logits:
+      logits = [row[int(l):] for row, l in zip(state.logits_buffer,
+                                               pad_lengths)]
+    return SamplerOutput(
+        text=[self.vocab.DecodeIds(t.tolist()) for t in toks],
+        logits=logits, tokens=toks)

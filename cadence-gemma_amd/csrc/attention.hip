@@ -1,0 +1,591 @@
+// Attention kernels for gfx950.
+//
+// flash_attn_kernel<HD, MODE>: one workgroup = 4 waves = 64 query rows of one
+// (batch, head); each wave owns 16 rows.  Key tiles of 32 are staged in LDS
+// (K row-major with an XOR chunk swizzle, V transposed so PV B-fragments are
+// 16-byte reads), S = Q.K^T and O += P.V run on mfma_f32_16x16x32_bf16,
+// softmax is online in fp32, P goes through a 1 KiB per-wave LDS tile to
+// become the next MFMA's A operand.
+//   MODE_LOCAL: Griffin local attention (modules.py:466-480): logits rounded
+//     to bf16 then * hd^-0.5, mask = same segment & causal & window; key
+//     tiles outside [max(seg_start, q0 - W), q_last] are skipped.  MQA: every
+//     head reads the single K/V head.
+//   MODE_VIT: timm bidirectional SDPA (fp32 logits, no mask but the tail).
+// decode_attn_kernel: one wave per sequence, 16 rows = the query heads,
+// keys = ring-buffer slots (positions of _compute_cache_mask) + the new key,
+// then the in-place slot update of _update_attention_cache.
+#include "common.hpp"
+#include "../../include/cadence_kernels.h"
+
+namespace {
+
+constexpr int MODE_LOCAL = 0;
+constexpr int MODE_VIT = 1;
+constexpr int KT = 32;  // keys per tile
+
+struct AttnArgs {
+  const u16* q; int64_t q_bs, q_rs, q_hs;   // batch / row / head strides
+  const u16* k; int64_t k_bs, k_rs, k_hs;
+  const u16* v; int64_t v_bs, v_rs, v_hs;
+  u16* o; int64_t o_bs, o_rs, o_hs;
+  const int32_t* seg; const int32_t* seg_start;
+  int L;          // query rows == key rows per sequence
+  int H, hd;      // heads, true head dim (<= HD)
+  int window;
+  float scale;
+};
+
+// XOR swizzle of a 16-B chunk index inside one K row; stays inside the row
+// for any chunks-per-row that is a multiple of 4 (HD = 96 -> 12 chunks).
+template <int CPR>
+CADENCE_DEV int swz(int ch, int row) {
+  return (CPR % 8 == 0) ? (ch ^ (row & 7)) : (ch ^ (row & 3));
+}
+
+template <int HD>
+struct Smem {
+  uint4 k[KT * HD / 8];        // [key][HD] swizzled 16-B chunks
+  u16 vt[HD * KT];             // [dim][key]
+  u16 p[4][16 * KT];           // per-wave P tile [row][key]
+};
+
+template <int HD, int MODE>
+__global__ __launch_bounds__(256) void flash_attn_kernel(AttnArgs a) {
+  constexpr int KS = HD / 32;   // k-steps for Q.K^T
+  constexpr int NO = HD / 16;   // output column reps
+  constexpr int CPR = HD / 8;   // 16-B chunks per K row
+  __shared__ Smem<HD> sm;
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int q0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qw = q0 + wave * 16;
+
+  const u16* qb = a.q + b * a.q_bs + h * a.q_hs;
+  const u16* kb = a.k + b * a.k_bs + h * a.k_hs;
+  const u16* vb = a.v + b * a.v_bs + h * a.v_hs;
+
+  // Q fragments: lane holds Q[row lane&15][32*ks + 8*(lane>>4) + j]
+  bf16x8 qf[KS];
+  {
+    const int r = qw + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int d = ks * 32 + 8 * (lane >> 4);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (r < a.L && d < a.hd) v = ld16(qb + (int64_t)r * a.q_rs + d);
+      qf[ks] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+
+  f32x4 o[NO];
+#pragma unroll
+  for (int j = 0; j < NO; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[4], l_run[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m_run[r] = -INFINITY;
+    l_run[r] = 0.0f;
+  }
+
+  // key range for the whole workgroup
+  int kbeg = 0, kend = a.L;
+  if (MODE == MODE_LOCAL) {
+    const int qlast = min(q0 + 63, a.L - 1);
+    int lo = a.seg_start[(int64_t)b * a.L + q0];
+    lo = max(lo, q0 - a.window);
+    kbeg = (max(lo, 0) / KT) * KT;
+    kend = qlast + 1;
+  }
+  const int rowq0 = qw + 4 * (lane >> 4);  // + r
+  int segq[4];
+  if (MODE == MODE_LOCAL) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qi = min(rowq0 + r, a.L - 1);
+      segq[r] = a.seg[(int64_t)b * a.L + qi];
+    }
+  }
+
+  for (int k0 = kbeg; k0 < kend; k0 += KT) {
+    __syncthreads();  // previous tile fully consumed
+    // stage K tile (swizzled) and V^T tile
+    for (int c = tid; c < KT * CPR; c += 256) {
+      const int kr = c / CPR, ch = c % CPR;
+      const int key = k0 + kr;
+      const int d = ch * 8;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (key < a.L && d < a.hd) {
+        kv = ld16(kb + (int64_t)key * a.k_rs + d);
+        vv = ld16(vb + (int64_t)key * a.v_rs + d);
+      }
+      sm.k[kr * CPR + swz<CPR>(ch, kr)] = kv;
+      const u16* vs = reinterpret_cast<const u16*>(&vv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sm.vt[(d + i) * KT + kr] = vs[i];
+    }
+    __syncthreads();
+
+    // S = Q K^T  (2 column reps of 16 keys)
+    f32x4 s[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int kr = jn * 16 + (lane & 15);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int ch = ks * 4 + (lane >> 4);
+        const bf16x8 kf = __builtin_bit_cast(bf16x8, sm.k[kr * CPR + swz<CPR>(ch, kr)]);
+        s[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, s[jn], 0, 0, 0);
+      }
+    }
+
+    // scale + mask, online softmax
+    float p[2][4];
+    float tmax[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tmax[r] = -INFINITY;
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int key = k0 + jn * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v;
+        bool ok;
+        if (MODE == MODE_LOCAL) {
+          v = rbf(s[jn][r]) * a.scale;
+          const int qi = rowq0 + r;
+          ok = key < a.L && key <= qi && qi <= key + a.window &&
+               a.seg[(int64_t)b * a.L + min(key, a.L - 1)] == segq[r];
+        } else {
+          v = s[jn][r] * a.scale;
+          ok = key < a.L;
+        }
+        v = ok ? v : -INFINITY;
+        p[jn][r] = v;
+        tmax[r] = fmaxf(tmax[r], v);
+      }
+    }
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float t = tmax[r];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) t = fmaxf(t, __shfl_xor(t, off, 64));
+      const float mn = fmaxf(m_run[r], t);
+      alpha[r] = (mn == -INFINITY) ? 1.0f : expf(m_run[r] - mn);
+      float rs = 0.0f;
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) {
+        const float e = (mn == -INFINITY) ? 0.0f : expf(p[jn][r] - mn);
+        p[jn][r] = e;
+        rs += e;
+      }
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off, 64);
+      l_run[r] = l_run[r] * alpha[r] + rs;
+      m_run[r] = mn;
+    }
+#pragma unroll
+    for (int j = 0; j < NO; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[j][r] *= alpha[r];
+
+    // P (bf16) -> LDS [row][key] -> A fragments
+    u16* pw = sm.p[wave];
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        pw[(4 * (lane >> 4) + r) * KT + jn * 16 + (lane & 15)] = f2bf(p[jn][r]);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const bf16x8 pf = __builtin_bit_cast(
+        bf16x8, *reinterpret_cast<const uint4*>(pw + (lane & 15) * KT + 8 * (lane >> 4)));
+#pragma unroll
+    for (int j = 0; j < NO; ++j) {
+      const bf16x8 vf = __builtin_bit_cast(
+          bf16x8, *reinterpret_cast<const uint4*>(&sm.vt[(j * 16 + (lane & 15)) * KT +
+                                                        8 * (lane >> 4)]));
+      o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[j], 0, 0, 0);
+    }
+  }
+
+  // normalise and store
+  u16* ob = a.o + b * a.o_bs + h * a.o_hs;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qi = rowq0 + r;
+    if (qi >= a.L) continue;
+    const float inv = l_run[r] > 0.0f ? 1.0f / l_run[r] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < NO; ++j) {
+      const int d = j * 16 + (lane & 15);
+      if (d < a.hd) ob[(int64_t)qi * a.o_rs + d] = f2bf(o[j][r] * inv);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ decode
+
+struct DecodeArgs {
+  const u16* q;           // [B, H*hd]
+  const u16* k_new;       // [B, hd] (row stride knew_rs)
+  const u16* v_new;
+  int64_t new_rs;
+  u16* ck; u16* cv;       // [B, W, hd]
+  int32_t* num_tokens;    // [B]
+  u16* o;                 // [B, H*hd]
+  int H, hd, W;
+  float scale;
+};
+
+template <int HD>
+__global__ __launch_bounds__(64) void decode_attn_kernel(DecodeArgs a) {
+  constexpr int KS = HD / 32, NO = HD / 16, CPR = HD / 8;
+  __shared__ uint4 ks_[KT * HD / 8];
+  __shared__ u16 vt[HD * KT];
+  __shared__ u16 pt[16 * KT];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int nt = a.num_tokens[b];
+  const int qpos = nt;
+  const int kblk = nt / a.W;
+  const int nslots = a.W + 1;  // ring slots + the new key
+  // slots with a non-negative position: all of them once the ring wrapped
+  const int slot_hi = nt >= a.W ? a.W : nt;
+
+  bf16x8 qf[KS];
+  {
+    const int hrow = lane & 15;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int d = ks * 32 + 8 * (lane >> 4);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (hrow < a.H) v = ld16(a.q + (int64_t)b * a.H * a.hd + hrow * a.hd + d);
+      qf[ks] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  f32x4 o[NO];
+#pragma unroll
+  for (int j = 0; j < NO; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[4], l_run[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m_run[r] = -INFINITY;
+    l_run[r] = 0.0f;
+  }
+  const u16* ckb = a.ck + (int64_t)b * a.W * a.hd;
+  const u16* cvb = a.cv + (int64_t)b * a.W * a.hd;
+
+  // iterate tiles over [0, slot_hi) and the final tile holding the new key
+  for (int k0 = 0; k0 < nslots; k0 += KT) {
+    if (k0 >= slot_hi && k0 + KT <= a.W) continue;  // no valid slot in tile
+    __syncthreads();
+    for (int c = lane; c < KT * CPR; c += 64) {
+      const int kr = c / CPR, ch = c % CPR;
+      const int slot = k0 + kr;
+      const int d = ch * 8;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (slot < a.W) {
+        kv = ld16(ckb + (int64_t)slot * a.hd + d);
+        vv = ld16(cvb + (int64_t)slot * a.hd + d);
+      } else if (slot == a.W) {
+        kv = ld16(a.k_new + (int64_t)b * a.new_rs + d);
+        vv = ld16(a.v_new + (int64_t)b * a.new_rs + d);
+      }
+      ks_[kr * CPR + swz<CPR>(ch, kr)] = kv;
+      const u16* vs = reinterpret_cast<const u16*>(&vv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) vt[(d + i) * KT + kr] = vs[i];
+    }
+    __syncthreads();
+    f32x4 s[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int kr = jn * 16 + (lane & 15);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int ch = ks * 4 + (lane >> 4);
+        const bf16x8 kf = __builtin_bit_cast(bf16x8, ks_[kr * CPR + swz<CPR>(ch, kr)]);
+        s[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, s[jn], 0, 0, 0);
+      }
+    }
+    float p[2][4], tmax[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tmax[r] = -INFINITY;
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int slot = k0 + jn * 16 + (lane & 15);
+      // _compute_cache_mask: slot positions from num_tokens
+      int kpos;
+      if (slot < a.W) {
+        const int now = slot + kblk * a.W;
+        kpos = now < nt ? now : slot + (kblk - 1) * a.W;
+      } else {
+        kpos = qpos;
+      }
+      const bool ok = slot <= a.W && kpos >= 0 && qpos >= kpos &&
+                      qpos <= kpos + a.W;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = ok ? rbf(s[jn][r]) * a.scale : -INFINITY;
+        p[jn][r] = v;
+        tmax[r] = fmaxf(tmax[r], v);
+      }
+    }
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float t = tmax[r];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) t = fmaxf(t, __shfl_xor(t, off, 64));
+      const float mn = fmaxf(m_run[r], t);
+      alpha[r] = (mn == -INFINITY) ? 1.0f : expf(m_run[r] - mn);
+      float rs = 0.0f;
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) {
+        const float e = (mn == -INFINITY) ? 0.0f : expf(p[jn][r] - mn);
+        p[jn][r] = e;
+        rs += e;
+      }
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off, 64);
+      l_run[r] = l_run[r] * alpha[r] + rs;
+      m_run[r] = mn;
+    }
+#pragma unroll
+    for (int j = 0; j < NO; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[j][r] *= alpha[r];
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        pt[(4 * (lane >> 4) + r) * KT + jn * 16 + (lane & 15)] = f2bf(p[jn][r]);
+    __syncthreads();
+    const bf16x8 pf = __builtin_bit_cast(
+        bf16x8, *reinterpret_cast<const uint4*>(pt + (lane & 15) * KT + 8 * (lane >> 4)));
+#pragma unroll
+    for (int j = 0; j < NO; ++j) {
+      const bf16x8 vf = __builtin_bit_cast(
+          bf16x8, *reinterpret_cast<const uint4*>(&vt[(j * 16 + (lane & 15)) * KT +
+                                                     8 * (lane >> 4)]));
+      o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int hrow = 4 * (lane >> 4) + r;
+    if (hrow >= a.H) continue;
+    const float inv = l_run[r] > 0.0f ? 1.0f / l_run[r] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < NO; ++j) {
+      const int d = j * 16 + (lane & 15);
+      a.o[(int64_t)b * a.H * a.hd + hrow * a.hd + d] = f2bf(o[j][r] * inv);
+    }
+  }
+  // _update_attention_cache: write the new key/value into slot nt % W, then
+  // bump num_tokens (all reads of this sequence's cache are done).
+  __syncthreads();
+  const int slot = nt % a.W;
+  for (int d = lane * 8; d < a.hd; d += 512) {
+    st16(a.ck + ((int64_t)b * a.W + slot) * a.hd + d,
+         ld16(a.k_new + (int64_t)b * a.new_rs + d));
+    st16(a.cv + ((int64_t)b * a.W + slot) * a.hd + d,
+         ld16(a.v_new + (int64_t)b * a.new_rs + d));
+  }
+  if (lane == 0) a.num_tokens[b] = nt + 1;
+}
+
+// ------------------------------------------------------------------- RoPE
+
+// One thread: 8 rotation pairs (16-B loads) of one head of one row, plus
+// the matching 16 pass-through dims.  Heads 0..H-1 are queries, head H is
+// the key; v is copied by head H's threads.
+__global__ __launch_bounds__(256) void rope_qkv_kernel(
+    const u16* __restrict__ qkv, int64_t ld, const int32_t* __restrict__ pos,
+    u16* __restrict__ qo, u16* __restrict__ ko, u16* __restrict__ vo, int64_t M,
+    int H, int hd) {
+  const int half = hd / 2, quarter = hd / 4;  // rope dims, pairs
+  const int cpq = quarter / 8;                // threads per head
+  const int64_t total = M * (H + 1) * cpq;
+  for (int64_t idx = blockIdx.x * 256 + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * 256) {
+    const int c = idx % cpq;
+    const int64_t mh = idx / cpq;
+    const int hh = mh % (H + 1);
+    const int64_t m = mh / (H + 1);
+    const u16* src = qkv + m * ld + hh * hd;
+    u16* dst = hh < H ? qo + m * (int64_t)H * hd + hh * hd : ko + m * hd;
+    const int i0 = c * 8;
+    float x1[8], x2[8];
+    unpack8(ld16(src + i0), x1);
+    unpack8(ld16(src + quarter + i0), x2);
+    const float p = (float)pos[m];
+    float o1[8], o2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int fi = i0 + i;
+      const float expo = (float)(2 * fi) / (float)half;
+      const float timescale = (float)pow(10000.0, (double)expo);
+      const float inv = 1.0f / timescale;
+      const float ang = p * inv;
+      const float sn = rbf((float)sin((double)ang));
+      const float cs = rbf((float)cos((double)ang));
+      o1[i] = bsub(bmul(x1[i], cs), bmul(x2[i], sn));
+      o2[i] = badd(bmul(x2[i], cs), bmul(x1[i], sn));
+    }
+    st16(dst + i0, pack8(o1));
+    st16(dst + quarter + i0, pack8(o2));
+    // pass-through half: this thread copies dims [half + 2*i0*?..)
+    const int pt_per = (hd - half) / cpq;  // dims per thread
+    for (int d = half + c * pt_per; d < half + (c + 1) * pt_per; d += 8)
+      st16(dst + d, ld16(src + d));
+    if (hh == H) {
+      const u16* vs = qkv + m * ld + (H + 1) * hd;
+      for (int d = c * (hd / cpq); d < (c + 1) * (hd / cpq); d += 8)
+        st16(vo + m * hd + d, ld16(vs + d));
+    }
+  }
+}
+
+// KV cache from the prompt: slot (i + num_tokens) % W <- key L - w + i.
+__global__ __launch_bounds__(256) void kv_fill_kernel(
+    const u16* __restrict__ k, const u16* __restrict__ v,
+    const int32_t* __restrict__ pos, u16* __restrict__ ck, u16* __restrict__ cv,
+    int32_t* __restrict__ ntok, int B, int L, int hd, int W) {
+  const int cpr = hd / 8;
+  const int64_t total = (int64_t)B * W * cpr;
+  for (int64_t idx = blockIdx.x * 256 + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * 256) {
+    const int c = idx % cpr;
+    const int64_t bs = idx / cpr;
+    const int slot = bs % W, b = bs / W;
+    const int nt = pos[(int64_t)b * L + L - 1] + 1;
+    const int w = L < W ? L : W;
+    // rolled[slot] = keys_tail[(slot - shift) mod w] for slot < w, else 0
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = kv;
+    if (slot < w) {
+      const int shift = ((nt % W) + W) % W;
+      int src = (slot - shift) % w;
+      if (src < 0) src += w;
+      const int64_t row = (int64_t)b * L + (L - w) + src;
+      kv = ld16(k + row * hd + c * 8);
+      vv = ld16(v + row * hd + c * 8);
+    }
+    st16(ck + ((int64_t)b * W + slot) * hd + c * 8, kv);
+    st16(cv + ((int64_t)b * W + slot) * hd + c * 8, vv);
+    if (slot == 0 && c == 0) ntok[b] = nt;
+  }
+}
+
+int grid_cap(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  if (g < 1) g = 1;
+  if (g > 8192) g = 8192;
+  return (int)g;
+}
+
+template <int HD, int MODE>
+void launch_flash(const AttnArgs& a, int B, hipStream_t st) {
+  dim3 grid((unsigned)((a.L + 63) / 64), (unsigned)a.H, (unsigned)B);
+  hipLaunchKernelGGL((flash_attn_kernel<HD, MODE>), grid, dim3(256), 0, st, a);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cadence_rope_qkv(const void* qkv, int64_t ldqkv, const int32_t* positions,
+                     void* q_out, void* k_out, void* v_out, int64_t M,
+                     int64_t H, int64_t hd, void* stream) {
+  if (hd % 64 || ldqkv % 8) return (int)hipErrorInvalidValue;
+  if (M <= 0) return 0;
+  const int cpq = (int)(hd / 4 / 8);
+  hipLaunchKernelGGL(rope_qkv_kernel, dim3(grid_cap(M * (H + 1) * cpq)), dim3(256),
+                     0, static_cast<hipStream_t>(stream),
+                     static_cast<const u16*>(qkv), ldqkv, positions,
+                     static_cast<u16*>(q_out), static_cast<u16*>(k_out),
+                     static_cast<u16*>(v_out), M, (int)H, (int)hd);
+  return (int)hipGetLastError();
+}
+
+int cadence_local_attention(const void* q, const void* k, const void* v,
+                            const int32_t* seg_id, const int32_t* seg_start,
+                            void* out, int64_t B, int64_t L, int64_t H,
+                            int64_t hd, int64_t window, void* stream) {
+  if (hd != 256 && hd != 128 && hd != 64) return (int)hipErrorInvalidValue;
+  if (B <= 0 || L <= 0) return 0;
+  AttnArgs a{};
+  a.q = static_cast<const u16*>(q); a.q_bs = L * H * hd; a.q_rs = H * hd; a.q_hs = hd;
+  a.k = static_cast<const u16*>(k); a.k_bs = L * hd; a.k_rs = hd; a.k_hs = 0;
+  a.v = static_cast<const u16*>(v); a.v_bs = L * hd; a.v_rs = hd; a.v_hs = 0;
+  a.o = static_cast<u16*>(out); a.o_bs = L * H * hd; a.o_rs = H * hd; a.o_hs = hd;
+  a.seg = seg_id; a.seg_start = seg_start;
+  a.L = (int)L; a.H = (int)H; a.hd = (int)hd; a.window = (int)window;
+  a.scale = 1.0f / sqrtf((float)hd);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (hd == 256) launch_flash<256, MODE_LOCAL>(a, (int)B, st);
+  else if (hd == 128) launch_flash<128, MODE_LOCAL>(a, (int)B, st);
+  else launch_flash<64, MODE_LOCAL>(a, (int)B, st);
+  return (int)hipGetLastError();
+}
+
+int cadence_vit_attention(const void* qkv, void* out, int64_t B, int64_t N,
+                          int64_t H, int64_t hd, void* stream) {
+  if (hd != 64 && hd != 72) return (int)hipErrorInvalidValue;
+  if (B <= 0 || N <= 0) return 0;
+  const int64_t D = H * hd;
+  AttnArgs a{};
+  const u16* base = static_cast<const u16*>(qkv);
+  a.q = base; a.q_bs = N * 3 * D; a.q_rs = 3 * D; a.q_hs = hd;
+  a.k = base + D; a.k_bs = N * 3 * D; a.k_rs = 3 * D; a.k_hs = hd;
+  a.v = base + 2 * D; a.v_bs = N * 3 * D; a.v_rs = 3 * D; a.v_hs = hd;
+  a.o = static_cast<u16*>(out); a.o_bs = N * D; a.o_rs = D; a.o_hs = hd;
+  a.L = (int)N; a.H = (int)H; a.hd = (int)hd; a.window = 0;
+  a.scale = 1.0f / sqrtf((float)hd);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (hd == 64) launch_flash<64, MODE_VIT>(a, (int)B, st);
+  else launch_flash<96, MODE_VIT>(a, (int)B, st);
+  return (int)hipGetLastError();
+}
+
+int cadence_kv_cache_fill(const void* k, const void* v,
+                          const int32_t* segment_pos, void* cache_k,
+                          void* cache_v, int32_t* num_tokens, int64_t B,
+                          int64_t L, int64_t hd, int64_t window, void* stream) {
+  if (hd % 8) return (int)hipErrorInvalidValue;
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(kv_fill_kernel, dim3(grid_cap(B * window * (hd / 8))), dim3(256),
+                     0, static_cast<hipStream_t>(stream),
+                     static_cast<const u16*>(k), static_cast<const u16*>(v),
+                     segment_pos, static_cast<u16*>(cache_k),
+                     static_cast<u16*>(cache_v), num_tokens, (int)B, (int)L,
+                     (int)hd, (int)window);
+  return (int)hipGetLastError();
+}
+
+int cadence_local_attention_decode(const void* q, const void* k_new,
+                                   const void* v_new, void* cache_k,
+                                   void* cache_v, int32_t* num_tokens,
+                                   void* out, int64_t B, int64_t H,
+                                   int64_t hd, int64_t window, void* stream) {
+  if ((hd != 256 && hd != 128 && hd != 64) || H > 16)
+    return (int)hipErrorInvalidValue;
+  if (B <= 0) return 0;
+  DecodeArgs a{static_cast<const u16*>(q), static_cast<const u16*>(k_new),
+               static_cast<const u16*>(v_new), hd,
+               static_cast<u16*>(cache_k), static_cast<u16*>(cache_v),
+               num_tokens, static_cast<u16*>(out), (int)H, (int)hd,
+               (int)window, 1.0f / sqrtf((float)hd)};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (hd == 256)
+    hipLaunchKernelGGL(decode_attn_kernel<256>, dim3((unsigned)B), dim3(64), 0, st, a);
+  else if (hd == 128)
+    hipLaunchKernelGGL(decode_attn_kernel<128>, dim3((unsigned)B), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(decode_attn_kernel<64>, dim3((unsigned)B), dim3(64), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

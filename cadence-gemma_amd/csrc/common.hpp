@@ -1,0 +1,90 @@
+// Shared device helpers for the CadenceGemma gfx950 kernels.
+//
+// Storage is bf16 (raw 16-bit in HBM), arithmetic is fp32 with explicit
+// bf16 rounding points where the reference rounds.
+// No FMA contraction is allowed where the reference performs separate eager
+// ops (see `mul_rn` / `add_rn`).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16;
+
+#define CADENCE_DEV __device__ __forceinline__
+
+CADENCE_DEV float bf2f(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+CADENCE_DEV float bf2f(bf16 v) { return (float)v; }
+// Round-to-nearest-even fp32 -> bf16 (v_cvt_pk_bf16_f32 on gfx950; keeps NaN).
+CADENCE_DEV u16 f2bf(float f) {
+  bf16 h = (bf16)f;
+  return __builtin_bit_cast(u16, h);
+}
+// Round an fp32 value through bf16 and back (one reference rounding point).
+CADENCE_DEV float rbf(float f) { return bf2f(f2bf(f)); }
+
+// Separate IEEE multiply / add (the reference's eager ops never fuse).
+CADENCE_DEV float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+CADENCE_DEV float add_rn(float a, float b) { return __fadd_rn(a, b); }
+CADENCE_DEV float sub_rn(float a, float b) { return __fsub_rn(a, b); }
+
+// bf16 elementwise ops as torch computes them for bf16 tensors: promote to
+// fp32, compute, round once.
+CADENCE_DEV float bmul(float a, float b) { return rbf(mul_rn(a, b)); }
+CADENCE_DEV float badd(float a, float b) { return rbf(add_rn(a, b)); }
+CADENCE_DEV float bsub(float a, float b) { return rbf(sub_rn(a, b)); }
+
+CADENCE_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+CADENCE_DEV float softplusf_(float x) {
+  // torch softplus(beta=1, threshold=20)
+  return x > 20.0f ? x : log1pf(expf(x));
+}
+CADENCE_DEV float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+CADENCE_DEV float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
+  const float k1 = 0.044715f;
+  float inner = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.0f + tanhf(inner));
+}
+
+// 16-byte vector of 8 bf16 (raw) for global/LDS traffic.
+struct alignas(16) u16x8 {
+  u16 v[8];
+};
+
+CADENCE_DEV uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+CADENCE_DEV void st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+
+CADENCE_DEV void unpack8(uint4 v, float (&f)[8]) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+CADENCE_DEV uint4 pack8(const float (&f)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+CADENCE_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+CADENCE_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+#define CADENCE_CHECK_LAUNCH() return (int)hipGetLastError()

@@ -1,0 +1,626 @@
+// bf16 MFMA GEMMs for gfx950 with the fused epilogues of the CadenceGemma
+// forward path.
+//
+//   C[M, N] = A[M, K] . W[N, K]^T       (both operands K-contiguous)
+//
+// Two engines:
+//  * tile engine (prefill, M > 64): 128x128x64 block tile, 4 waves (2x2),
+//    wave tile 64x64 = 4x4 mfma_f32_16x16x32_bf16, register-staged
+//    double-buffered LDS with an XOR chunk swizzle (conflict-free
+//    ds_read_b128 / ds_write_b128), XCD-aware bijective block remap and a
+//    grouped tile order for L2 reuse.
+//  * skinny engine (decode, M <= 64): weight rows streamed once straight into
+//    MFMA B fragments, split-K over the grid, fp32 partial slabs reduced in a
+//    fixed order (deterministic) by a second kernel that applies the same
+//    epilogue.
+//
+// Epilogues replicate the reference rounding points:
+//  EpiLinear      nn.Linear (+bias) [+GELU(erf)] [+residual], row remap
+//  EpiGatedGelu   MLPBlock: gelu_tanh(x.Wg + bg) * (x.Wu + bu)  modules.py:754-756
+//  EpiRglruGates  RG-LRU gate chain -> (a, normalized_x)       layers.py:345-365
+//  EpiVitResid    timm residual: resid += gamma * (x.W + b)   (fp32 stream)
+//  EpiPatch       patch-embed conv as GEMM + pos_embed at a prefix offset
+#include "common.hpp"
+#include "../../include/cadence_kernels.h"
+
+namespace {
+
+constexpr int BK = 64;
+
+// ---------------------------------------------------------------- epilogues
+
+struct RowMap {
+  int64_t div, mul, off;  // out_row = (m / div) * mul + (m % div) + off
+  CADENCE_DEV int64_t operator()(int64_t m) const {
+    return (m / div) * mul + (m % div) + off;
+  }
+};
+
+// griffin.py:219-221 on bf16 logits: tanh(l / c) * c, each op rounded.
+CADENCE_DEV float softcap(float l, float c) {
+  const float t = rbf(l / c);
+  return rbf(rbf(tanhf(t)) * c);
+}
+
+struct EpiLinear {
+  static constexpr bool kPaired = false;
+  u16* out; int64_t ldo;
+  const u16* bias;
+  const u16* resid; int64_t ldr;
+  int act;                 // 0 none, 1 gelu(erf), 2 soft-cap(cap), 3 gelu(tanh)
+  RowMap map;
+  float cap;
+  CADENCE_DEV void apply(int64_t m, int n, float v, int) const {
+    // F.linear adds the bias in fp32 before the single bf16 rounding.
+    if (bias) v = add_rn(v, bf2f(bias[n]));
+    float r = rbf(v);
+    if (act == 1) r = rbf(gelu_erf(r));
+    if (act == 2) r = softcap(r, cap);
+    if (act == 3) r = rbf(gelu_tanh(r));
+    const int64_t orow = map(m);
+    if (resid) r = badd(r, bf2f(resid[orow * ldr + n]));
+    out[orow * ldo + n] = f2bf(r);
+  }
+};
+
+struct EpiGatedGelu {
+  static constexpr bool kPaired = true;
+  u16* out; int64_t ldo;
+  const u16* bias_g; const u16* bias_u;
+  CADENCE_DEV void apply2(int64_t m, int f, float g, float u, int) const {
+    // Einsum result is rounded, then `+ b` rounds again (layers.py:729).
+    g = badd(rbf(g), bf2f(bias_g[f]));
+    u = badd(rbf(u), bf2f(bias_u[f]));
+    out[m * ldo + f] = f2bf(bmul(rbf(gelu_tanh(g)), u));
+  }
+};
+
+struct EpiRglruGates {
+  static constexpr bool kPaired = true;
+  const u16* x; int64_t ldx;         // conv1d output (RG-LRU input)
+  const u16* bias_x; const u16* bias_a;
+  const u16* softplus_a;             // bf16(softplus(a_param)), [E]
+  const int32_t* segpos;             // [M]
+  u16* a_out; u16* nx_out; int64_t ldo;
+  int bw;                            // block width (256)
+  CADENCE_DEV void apply2(int64_t m, int j, float accx, float acca, int g) const {
+    const int e = g * bw + j;
+    const float gx = rbf(sigmoidf_(badd(rbf(accx), bf2f(bias_x[e]))));
+    const float ga = rbf(sigmoidf_(badd(rbf(acca), bf2f(bias_a[e]))));
+    const float log_a = bmul(rbf(-8.0f * ga), bf2f(softplus_a[e]));
+    const float a = rbf(expf(log_a));
+    const float a_sq = rbf(expf(rbf(2.0f * log_a)));
+    const float gated = bmul(bf2f(x[m * ldx + e]), gx);
+    const bool reset = segpos[m] == 0;
+    const float mult = reset ? 1.0f : rbf(sqrtf(rbf(1.0f - a_sq)));
+    a_out[m * ldo + e] = f2bf(reset ? 0.0f : a);
+    nx_out[m * ldo + e] = f2bf(bmul(gated, mult));
+  }
+};
+
+struct EpiVitResid {
+  static constexpr bool kPaired = false;
+  float* resid; int64_t ldr;
+  const u16* bias; const u16* gamma;
+  CADENCE_DEV void apply(int64_t m, int n, float v, int) const {
+    v += bf2f(bias[n]);
+    if (gamma) v *= bf2f(gamma[n]);
+    resid[m * ldr + n] += v;
+  }
+};
+
+struct EpiPatch {
+  static constexpr bool kPaired = false;
+  float* resid;                      // [B, ntok, N] fp32
+  const u16* bias; const u16* pos;   // pos [P, N]
+  int64_t P, ntok, prefix, N;
+  CADENCE_DEV void apply(int64_t m, int n, float v, int) const {
+    const int64_t b = m / P, p = m % P;
+    v += bf2f(bias[n]);
+    v += bf2f(pos[p * N + n]);
+    resid[(b * ntok + prefix + p) * N + n] = v;
+  }
+};
+
+// Paired epilogues take the (gate, up) halves of each 64-column group:
+// packed column 64g + w (w < 32) pairs with 64g + 32 + w -> logical 32g + w.
+
+// ------------------------------------------------------------ tile engine
+
+template <int BM, int BN, class Epi>
+__global__ __launch_bounds__(256, 2) void gemm_tile_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
+    int64_t ldw, int M, int N, int K, int64_t a_goff, int64_t w_goff,
+    Epi epi) {
+  constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
+  constexpr int ACH = BM * 8 / 256, BCH = BN * 8 / 256;  // 16-B chunks/thread
+  __shared__ uint4 smem[2][(BM + BN) * 8];
+
+  const int g = blockIdx.y;
+  A += g * a_goff;
+  W += g * w_goff;
+
+  const int ntm = (M + BM - 1) / BM, ntn = N / BN, nt = ntm * ntn;
+  int t = blockIdx.x;
+  {  // bijective XCD remap: blocks sharing an XCD get a contiguous tile range
+    const int xcd = t & 7, q = nt >> 3, r = nt & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    t = base + (t >> 3);
+  }
+  constexpr int GM = 8;
+  const int grp = t / (GM * ntn), fm = grp * GM;
+  const int gs = min(ntm - fm, GM);
+  const int within = t % (GM * ntn);
+  const int tm = fm + within % gs, tn = within / gs;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lrow = tid >> 3, lch = tid & 7;
+
+  uint4 ra[ACH], rb[BCH];
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int r = lrow + 32 * i;
+      const int gr = m0 + r;
+      ra[i] = gr < M ? ld16(A + (int64_t)gr * lda + k0 + lch * 8) : zero;
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int r = lrow + 32 * i;
+      rb[i] = ld16(W + (int64_t)(n0 + r) * ldw + k0 + lch * 8);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int r = lrow + 32 * i;
+      smem[buf][r * 8 + (lch ^ (r & 7))] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int r = lrow + 32 * i;
+      smem[buf][(BM + r) * 8 + (lch ^ (r & 7))] = rb[i];
+    }
+  };
+
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[MR], bfr[NR];
+      const int ch = s * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        const int r = wm * WM + i * 16 + (lane & 15);
+        af[i] = __builtin_bit_cast(bf16x8, smem[cur][r * 8 + (ch ^ (r & 7))]);
+      }
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        const int r = wn * WN + j * 16 + (lane & 15);
+        bfr[j] = __builtin_bit_cast(bf16x8,
+                                    smem[cur][(BM + r) * 8 + (ch ^ (r & 7))]);
+      }
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j],
+                                                              acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // Epilogue: C/D layout of 16x16x32 -> col = lane & 15, row = 4*(lane>>4)+r.
+  const int mbase = m0 + wm * WM, nbase = n0 + wn * WN;
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+  if constexpr (Epi::kPaired) {
+    static_assert(NR == 4, "paired epilogue needs 64-column wave tiles");
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mbase + i * 16 + rsub + r;
+          if (row < M)
+            epi.apply2(row, nbase / 2 + j * 16 + csub, acc[i][j][r],
+                       acc[i][j + 2][r], g);
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mbase + i * 16 + rsub + r;
+          if (row < M) epi.apply(row, nbase + j * 16 + csub, acc[i][j][r], g);
+        }
+  }
+}
+
+// ---------------------------------------------------------- skinny engine
+
+// One block: 64 output columns x MS rows over one K split; 4 waves split the
+// K range round-robin in 32-deep steps and are summed through LDS.
+template <int MS>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
+    int64_t ldw, int M, int N, int K, int klen, float* __restrict__ part,
+    int64_t a_goff, int64_t w_goff) {
+  constexpr int MR = MS / 16;
+  constexpr int UNROLL = 2;
+  __shared__ float red[4][MS * 64];
+  const int g = blockIdx.z;
+  A += g * a_goff;
+  W += g * w_goff;
+  const int n0 = blockIdx.x * 64;
+  const int kbeg = blockIdx.y * klen;
+  const int kend = min(K, kbeg + klen);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int koff = 8 * (lane >> 4);
+
+  f32x4 acc[MR][4];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  for (int kk = kbeg + 32 * wave; kk < kend; kk += 32 * 4 * UNROLL) {
+    uint4 wb[UNROLL][4];
+    uint4 xa[UNROLL][MR];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = kk + u * 128;
+      const bool ok = k < kend;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        wb[u][j] = ok ? ld16(W + (int64_t)(n0 + j * 16 + (lane & 15)) * ldw + k + koff)
+                      : zero;
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        const int m = i * 16 + (lane & 15);
+        xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + k + koff) : zero;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, xa[u][i]),
+              __builtin_bit_cast(bf16x8, wb[u][j]), acc[i][j], 0, 0, 0);
+  }
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[wave][(i * 16 + rsub + r) * 64 + j * 16 + csub] = acc[i][j][r];
+  __syncthreads();
+  float* dst = part + ((int64_t)blockIdx.y * gridDim.z + g) * (int64_t)M * N;
+  for (int idx = tid; idx < MS * 64; idx += 256) {
+    const int m = idx / 64, n = idx % 64;
+    if (m < M) {
+      const float s = (red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx]);
+      dst[(int64_t)m * N + n0 + n] = s;
+    }
+  }
+}
+
+// Sums the split-K slabs in split order and applies the epilogue.
+template <class Epi>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(
+    const float* __restrict__ part, int splits, int groups, int M, int N,
+    Epi epi) {
+  const int g = blockIdx.y;
+  const int64_t slab = (int64_t)M * N;
+  if constexpr (Epi::kPaired) {
+    const int half = N / 2;
+    for (int64_t idx = blockIdx.x * 256 + threadIdx.x; idx < (int64_t)M * half;
+         idx += (int64_t)gridDim.x * 256) {
+      const int m = idx / half, oc = idx % half;
+      const int c0 = (oc / 32) * 64 + (oc % 32), c1 = c0 + 32;
+      float v0 = 0.f, v1 = 0.f;
+      for (int s = 0; s < splits; ++s) {
+        const float* p = part + ((int64_t)s * groups + g) * slab + (int64_t)m * N;
+        v0 += p[c0];
+        v1 += p[c1];
+      }
+      epi.apply2(m, oc, v0, v1, g);
+    }
+  } else {
+    for (int64_t idx = blockIdx.x * 256 + threadIdx.x; idx < (int64_t)M * N;
+         idx += (int64_t)gridDim.x * 256) {
+      const int m = idx / N, n = idx % N;
+      float v = 0.f;
+      for (int s = 0; s < splits; ++s)
+        v += part[((int64_t)s * groups + g) * slab + (int64_t)m * N + n];
+      epi.apply(m, n, v, g);
+    }
+  }
+}
+
+
+// Logits reduce: one block = 256 vocabulary columns of one row.  Applies the
+// soft-cap chain, optionally stores bf16 logits, and emits the block's
+// (max, lowest index) pair.
+__global__ __launch_bounds__(256) void logits_reduce_kernel(
+    const float* __restrict__ part, int splits, int M, int V, float cap,
+    u16* __restrict__ logits, float* __restrict__ bval, int* __restrict__ bidx) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int m = blockIdx.y;
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  float v = -INFINITY;
+  int idx = 0x7fffffff;
+  if (n < V) {
+    float acc = 0.f;
+    for (int s = 0; s < splits; ++s) acc += part[((int64_t)s * M + m) * V + n];
+    float l = rbf(acc);
+    if (cap > 0.0f) l = softcap(l, cap);
+    if (logits) logits[(int64_t)m * V + n] = f2bf(l);
+    v = l;
+    idx = n;
+  }
+  // wave argmax (ties -> lowest index)
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(v, off, 64);
+    const int oi = __shfl_xor(idx, off, 64);
+    if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sv[wave] = v; si[wave] = idx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (sv[w] > v || (sv[w] == v && si[w] < idx)) { v = sv[w]; idx = si[w]; }
+    bval[(int64_t)m * gridDim.x + blockIdx.x] = v;
+    bidx[(int64_t)m * gridDim.x + blockIdx.x] = idx;
+  }
+}
+
+__global__ __launch_bounds__(256) void argmax_final_kernel(
+    const float* __restrict__ bval, const int* __restrict__ bidx, int nblk,
+    int32_t* __restrict__ out) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int m = blockIdx.x;
+  float v = -INFINITY;
+  int idx = 0x7fffffff;
+  for (int i = threadIdx.x; i < nblk; i += 256) {
+    const float ov = bval[(int64_t)m * nblk + i];
+    const int oi = bidx[(int64_t)m * nblk + i];
+    if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(v, off, 64);
+    const int oi = __shfl_xor(idx, off, 64);
+    if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sv[wave] = v; si[wave] = idx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (sv[w] > v || (sv[w] == v && si[w] < idx)) { v = sv[w]; idx = si[w]; }
+    out[m] = idx;
+  }
+}
+
+constexpr int kSkinnyMaxM = 64;
+
+int skinny_splits(int64_t N, int64_t K, int64_t groups) {
+  const int64_t tiles = (N / 64) * groups;
+  const int64_t ksteps = K / 32;
+  // aim for ~512 blocks, keep >= 8 k-steps (2 per wave) per split
+  int64_t splits = (512 + tiles - 1) / tiles;
+  splits = splits < 1 ? 1 : splits;
+  const int64_t maxs = ksteps / 8 > 0 ? ksteps / 8 : 1;
+  if (splits > maxs) splits = maxs;
+  return (int)splits;
+}
+
+int64_t skinny_klen(int64_t K, int splits) {
+  int64_t klen = (K + splits - 1) / splits;
+  klen = (klen + 31) / 32 * 32;
+  return klen;
+}
+
+template <class Epi>
+int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
+                int64_t N, int64_t K, int64_t groups, int64_t a_goff,
+                int64_t w_goff, const Epi& epi, void* ws, int64_t ws_bytes,
+                hipStream_t st) {
+  if (M <= 0) return 0;
+  if (M > kSkinnyMaxM) {
+    if (N % 128 || K % BK) return (int)hipErrorInvalidValue;
+    const int64_t tiles = ((M + 127) / 128) * (N / 128);
+    dim3 grid((unsigned)tiles, (unsigned)groups);
+    hipLaunchKernelGGL((gemm_tile_kernel<128, 128, Epi>), grid, dim3(256), 0, st,
+                       A, lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
+    return (int)hipGetLastError();
+  }
+  if (N % 64 || K % 32) return (int)hipErrorInvalidValue;
+  const int splits = skinny_splits(N, K, groups);
+  const int64_t klen = skinny_klen(K, splits);
+  const int64_t need = (int64_t)splits * groups * M * N * 4;
+  if (!ws || ws_bytes < need) return (int)hipErrorInvalidValue;
+  float* part = static_cast<float*>(ws);
+  dim3 grid((unsigned)(N / 64), (unsigned)splits, (unsigned)groups);
+  if (M <= 16)
+    hipLaunchKernelGGL((gemm_skinny_kernel<16>), grid, dim3(256), 0, st, A, lda, W,
+                       ldw, (int)M, (int)N, (int)K, (int)klen, part, a_goff, w_goff);
+  else if (M <= 32)
+    hipLaunchKernelGGL((gemm_skinny_kernel<32>), grid, dim3(256), 0, st, A, lda, W,
+                       ldw, (int)M, (int)N, (int)K, (int)klen, part, a_goff, w_goff);
+  else
+    hipLaunchKernelGGL((gemm_skinny_kernel<64>), grid, dim3(256), 0, st, A, lda, W,
+                       ldw, (int)M, (int)N, (int)K, (int)klen, part, a_goff, w_goff);
+  int64_t outs = M * N;
+  int rblocks = (int)((outs + 255) / 256);
+  if (rblocks > 4096) rblocks = 4096;
+  hipLaunchKernelGGL((splitk_reduce_kernel<Epi>), dim3(rblocks, (unsigned)groups),
+                     dim3(256), 0, st, part, splits, (int)groups, (int)M, (int)N, epi);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+int cadence_abi_version(void) { return 1; }
+
+int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
+                                     int64_t groups) {
+  if (M > kSkinnyMaxM || M <= 0) return 0;
+  const int splits = skinny_splits(N, K, groups);
+  return (int64_t)splits * groups * M * N * 4;
+}
+
+int cadence_gemm_linear(const void* A, int64_t lda, const void* W, int64_t ldw,
+                        const void* bias, const void* resid, int64_t ld_resid,
+                        void* out, int64_t ldo, int64_t M, int64_t N, int64_t K,
+                        int act, int64_t row_div, int64_t row_mul,
+                        int64_t row_off, void* workspace, int64_t ws_bytes,
+                        void* stream) {
+  if (row_div <= 0) return (int)hipErrorInvalidValue;
+  EpiLinear epi{static_cast<u16*>(out), ldo, static_cast<const u16*>(bias),
+                static_cast<const u16*>(resid), ld_resid, act,
+                RowMap{row_div, row_mul, row_off}, 0.0f};
+  return launch_gemm(static_cast<const u16*>(A), lda, static_cast<const u16*>(W),
+                     ldw, M, N, K, 1, 0, 0, epi, workspace, ws_bytes,
+                     static_cast<hipStream_t>(stream));
+}
+
+int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
+                            const void* bias_gate, const void* bias_up,
+                            void* out, int64_t ldo, int64_t M, int64_t F,
+                            int64_t K, void* workspace, int64_t ws_bytes,
+                            void* stream) {
+  if (F % 64) return (int)hipErrorInvalidValue;
+  EpiGatedGelu epi{static_cast<u16*>(out), ldo,
+                   static_cast<const u16*>(bias_gate),
+                   static_cast<const u16*>(bias_up)};
+  return launch_gemm(static_cast<const u16*>(A), lda,
+                     static_cast<const u16*>(Wpacked), K, M, 2 * F, K, 1, 0, 0,
+                     epi, workspace, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
+                        const void* bias_x, const void* bias_a,
+                        const void* softplus_a, const int32_t* segment_pos,
+                        void* a_out, void* nx_out, int64_t ldo, int64_t M,
+                        int64_t heads, int64_t bw, void* workspace,
+                        int64_t ws_bytes, void* stream) {
+  if (bw % 64) return (int)hipErrorInvalidValue;
+  EpiRglruGates epi{static_cast<const u16*>(X), ldx,
+                    static_cast<const u16*>(bias_x),
+                    static_cast<const u16*>(bias_a),
+                    static_cast<const u16*>(softplus_a), segment_pos,
+                    static_cast<u16*>(a_out), static_cast<u16*>(nx_out), ldo,
+                    (int)bw};
+  return launch_gemm(static_cast<const u16*>(X), ldx,
+                     static_cast<const u16*>(Wpacked), bw, M, 2 * bw, bw, heads,
+                     bw, 2 * bw * bw, epi, workspace, ws_bytes,
+                     static_cast<hipStream_t>(stream));
+}
+
+int cadence_gemm_vit_residual(const void* A, int64_t lda, const void* W,
+                              int64_t ldw, const void* bias, const void* gamma,
+                              float* resid, int64_t ld_resid, int64_t M,
+                              int64_t N, int64_t K, void* workspace,
+                              int64_t ws_bytes, void* stream) {
+  EpiVitResid epi{resid, ld_resid, static_cast<const u16*>(bias),
+                  static_cast<const u16*>(gamma)};
+  return launch_gemm(static_cast<const u16*>(A), lda, static_cast<const u16*>(W),
+                     ldw, M, N, K, 1, 0, 0, epi, workspace, ws_bytes,
+                     static_cast<hipStream_t>(stream));
+}
+
+int cadence_gemm_patch_embed(const void* patches, int64_t ldp, const void* W,
+                             int64_t ldw, const void* bias, const void* pos,
+                             float* resid, int64_t B, int64_t P, int64_t ntok,
+                             int64_t prefix, int64_t N, int64_t K,
+                             void* workspace, int64_t ws_bytes, void* stream) {
+  EpiPatch epi{resid, static_cast<const u16*>(bias),
+               static_cast<const u16*>(pos), P, ntok, prefix, N};
+  return launch_gemm(static_cast<const u16*>(patches), ldp,
+                     static_cast<const u16*>(W), ldw, B * P, N, K, 1, 0, 0, epi,
+                     workspace, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+int64_t cadence_logits_scratch_bytes(int64_t M, int64_t V, int64_t D) {
+  const int splits = skinny_splits(V, D, 1);
+  const int64_t nblk = (V + 255) / 256;
+  return (int64_t)splits * M * V * 4 + M * nblk * 8 + 256;
+}
+
+int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
+                          int64_t M, int64_t V, int64_t D, float soft_cap,
+                          void* logits_out, int32_t* next_token,
+                          void* scratch, int64_t scratch_bytes, void* stream) {
+  if (M <= 0) return 0;
+  if (M > kSkinnyMaxM || V % 64 || D % 32) return (int)hipErrorInvalidValue;
+  if (scratch_bytes < cadence_logits_scratch_bytes(M, V, D))
+    return (int)hipErrorInvalidValue;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int splits = skinny_splits(V, D, 1);
+  const int64_t klen = skinny_klen(D, splits);
+  float* part = static_cast<float*>(scratch);
+  const int64_t nblk = (V + 255) / 256;
+  float* bval = part + (int64_t)splits * M * V;
+  int* bidx = reinterpret_cast<int*>(bval + M * nblk);
+  const u16* A = static_cast<const u16*>(X);
+  const u16* W = static_cast<const u16*>(E);
+  dim3 grid((unsigned)(V / 64), (unsigned)splits, 1);
+  if (M <= 16)
+    hipLaunchKernelGGL((gemm_skinny_kernel<16>), grid, dim3(256), 0, st, A, ldx, W,
+                       D, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0);
+  else if (M <= 32)
+    hipLaunchKernelGGL((gemm_skinny_kernel<32>), grid, dim3(256), 0, st, A, ldx, W,
+                       D, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0);
+  else
+    hipLaunchKernelGGL((gemm_skinny_kernel<64>), grid, dim3(256), 0, st, A, ldx, W,
+                       D, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0);
+  hipLaunchKernelGGL(logits_reduce_kernel, dim3((unsigned)nblk, (unsigned)M),
+                     dim3(256), 0, st, part, splits, (int)M, (int)V, soft_cap,
+                     static_cast<u16*>(logits_out), bval, bidx);
+  if (next_token)
+    hipLaunchKernelGGL(argmax_final_kernel, dim3((unsigned)M), dim3(256), 0, st,
+                       bval, bidx, (int)nblk, next_token);
+  return (int)hipGetLastError();
+}
+
+int cadence_gemm_logits(const void* X, int64_t ldx, const void* E, int64_t M,
+                        int64_t V, int64_t D, float soft_cap, void* out,
+                        int64_t ldo, void* workspace, int64_t ws_bytes,
+                        void* stream) {
+  EpiLinear epi{static_cast<u16*>(out), ldo, nullptr, nullptr, 0,
+                soft_cap > 0.0f ? 2 : 0, RowMap{M > 0 ? M : 1, 0, 0}, soft_cap};
+  return launch_gemm(static_cast<const u16*>(X), ldx, static_cast<const u16*>(E),
+                     D, M, V, D, 1, 0, 0, epi, workspace, ws_bytes,
+                     static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

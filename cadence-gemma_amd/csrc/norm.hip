@@ -1,0 +1,223 @@
+// Row-wise kernels: Griffin RMSNorm, ViT LayerNorm, token embedding, and the
+// small int bookkeeping kernels (image-splice positions, segment ids).
+// One wave per row, 16-byte vector accesses (G13), fp32 reductions.
+#include "common.hpp"
+#include "../../include/cadence_kernels.h"
+
+namespace {
+
+// layers.py:73-78 on bf16 tensors: square (rounded), mean (fp32 sum,
+// rounded), + eps (rounded), rsqrt (rounded), x * r (rounded),
+// scale + 1 (rounded), product (rounded).
+__global__ __launch_bounds__(256) void rmsnorm_kernel(
+    const u16* __restrict__ x, int64_t ldx, const u16* __restrict__ scale,
+    u16* __restrict__ out, int64_t ldo, int64_t rows, int width, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const u16* xr = x + row * ldx;
+  float ss = 0.0f;
+  for (int c = lane * 8; c < width; c += 512) {
+    float v[8];
+    unpack8(ld16(xr + c), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ss += rbf(v[i] * v[i]);
+  }
+  ss = wave_sum(ss);
+  const float var = rbf(ss / (float)width);
+  const float r = rbf(1.0f / sqrtf(rbf(var + eps)));
+  u16* orow = out + row * ldo;
+  for (int c = lane * 8; c < width; c += 512) {
+    float v[8], s[8];
+    unpack8(ld16(xr + c), v);
+    unpack8(ld16(scale + c), s);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = bmul(bmul(v[i], r), badd(s[i], 1.0f));
+    st16(orow + c, pack8(v));
+  }
+}
+
+// timm LayerNorm (eps 1e-6) over the fp32 residual stream, bf16 out.
+__global__ __launch_bounds__(256) void layernorm_kernel(
+    const float* __restrict__ x, int64_t ldx, const u16* __restrict__ w,
+    const u16* __restrict__ b, u16* __restrict__ out, int64_t ldo,
+    int64_t rows, int width, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * ldx;
+  float s = 0.0f;
+  for (int c = lane * 4; c < width; c += 256) {
+    const float4 v = *reinterpret_cast<const float4*>(xr + c);
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+  const float mean = wave_sum(s) / (float)width;
+  float q = 0.0f;
+  for (int c = lane * 4; c < width; c += 256) {
+    const float4 v = *reinterpret_cast<const float4*>(xr + c);
+    const float d0 = v.x - mean, d1 = v.y - mean, d2 = v.z - mean, d3 = v.w - mean;
+    q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)width + eps);
+  u16* orow = out + row * ldo;
+  for (int c = lane * 4; c < width; c += 256) {
+    const float4 v = *reinterpret_cast<const float4*>(xr + c);
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float y0 = (vv[2 * i] - mean) * rstd * bf2f(w[c + 2 * i]) + bf2f(b[c + 2 * i]);
+      const float y1 = (vv[2 * i + 1] - mean) * rstd * bf2f(w[c + 2 * i + 1]) +
+                       bf2f(b[c + 2 * i + 1]);
+      o[i] = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
+    }
+    *reinterpret_cast<uint2*>(orow + c) = make_uint2(o[0], o[1]);
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_kernel(
+    const int32_t* __restrict__ tok, const u16* __restrict__ E,
+    u16* __restrict__ out, int64_t ldo, int64_t M, int D, float scale,
+    int64_t div, int64_t mul, int64_t off) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const u16* src = E + (int64_t)tok[m] * D;
+  u16* dst = out + ((m / div) * mul + (m % div) + off) * ldo;
+  for (int c = lane * 8; c < D; c += 512) {
+    uint4 v = ld16(src + c);
+    if (scale != 1.0f) {
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = bmul(f[i], scale);
+      v = pack8(f);
+    }
+    st16(dst + c, v);
+  }
+}
+
+__global__ void splice_positions_kernel(const int32_t* __restrict__ text,
+                                        int32_t* __restrict__ out, int B, int T,
+                                        int n_vis) {
+  const int L = n_vis + T;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < (int64_t)B * L;
+       i += (int64_t)gridDim.x * 256) {
+    const int b = i / L, t = i % L;
+    out[i] = t < n_vis ? t : text[(int64_t)b * T + t - n_vis];
+  }
+}
+
+// seg_id = cumsum(pos == 0) (modules.py:145); seg_start = first index of
+// the row's segment.  One thread per sequence (L is at most a few thousand).
+__global__ void segment_info_kernel(const int32_t* __restrict__ pos,
+                                    int32_t* __restrict__ seg,
+                                    int32_t* __restrict__ start, int B, int L) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  int s = 0, st = 0;
+  for (int t = 0; t < L; ++t) {
+    if (pos[(int64_t)b * L + t] == 0) {
+      ++s;
+      st = t;
+    }
+    seg[(int64_t)b * L + t] = s;
+    start[(int64_t)b * L + t] = st;
+  }
+}
+
+// Greedy-decode bookkeeping on device (no host sync per step):
+// out[b, *step] = next[b]; pos[b] += 1; (++*step once).
+__global__ void decode_advance_kernel(const int32_t* __restrict__ next,
+                                      int32_t* __restrict__ out, int64_t ldo,
+                                      int32_t* __restrict__ step,
+                                      int32_t* __restrict__ pos, int B) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  const int s = *step;
+  if (b < B) {
+    out[(int64_t)b * ldo + s] = next[b];
+    pos[b] += 1;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) *step = s + 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cadence_decode_advance(const int32_t* next_token, int32_t* tokens_out,
+                           int64_t ld_out, int32_t* step, int32_t* positions,
+                           int64_t B, void* stream) {
+  if (B <= 0) return 0;
+  if (B > 256) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), next_token, tokens_out,
+                     ld_out, step, positions, (int)B);
+  return (int)hipGetLastError();
+}
+
+
+int cadence_rmsnorm(const void* x, int64_t ldx, const void* scale, void* out,
+                    int64_t ldo, int64_t rows, int64_t width, float eps,
+                    void* stream) {
+  if (width % 8 || ldx % 8 || ldo % 8) return (int)hipErrorInvalidValue;
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256),
+                     0, static_cast<hipStream_t>(stream),
+                     static_cast<const u16*>(x), ldx,
+                     static_cast<const u16*>(scale), static_cast<u16*>(out), ldo,
+                     rows, (int)width, eps);
+  return (int)hipGetLastError();
+}
+
+int cadence_layernorm(const float* x, int64_t ldx, const void* weight,
+                      const void* bias, void* out, int64_t ldo, int64_t rows,
+                      int64_t width, float eps, void* stream) {
+  if (width % 4 || ldx % 4 || ldo % 4) return (int)hipErrorInvalidValue;
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((rows + 3) / 4)),
+                     dim3(256), 0, static_cast<hipStream_t>(stream), x, ldx,
+                     static_cast<const u16*>(weight),
+                     static_cast<const u16*>(bias), static_cast<u16*>(out), ldo,
+                     rows, (int)width, eps);
+  return (int)hipGetLastError();
+}
+
+int cadence_embed(const int32_t* tokens, const void* E, void* out,
+                  int64_t ldo, int64_t M, int64_t D, float scale,
+                  int64_t row_div, int64_t row_mul, int64_t row_off,
+                  void* stream) {
+  if (D % 8 || ldo % 8 || row_div <= 0) return (int)hipErrorInvalidValue;
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), tokens,
+                     static_cast<const u16*>(E), static_cast<u16*>(out), ldo, M,
+                     (int)D, scale, row_div, row_mul, row_off);
+  return (int)hipGetLastError();
+}
+
+int cadence_splice_positions(const int32_t* text_pos, int32_t* out,
+                             int64_t B, int64_t T, int64_t n_vis,
+                             void* stream) {
+  const int64_t n = B * (n_vis + T);
+  if (n <= 0) return 0;
+  int64_t g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(splice_positions_kernel, dim3((unsigned)g), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), text_pos, out, (int)B,
+                     (int)T, (int)n_vis);
+  return (int)hipGetLastError();
+}
+
+int cadence_segment_info(const int32_t* segment_pos, int32_t* seg_id,
+                         int32_t* seg_start, int64_t B, int64_t L,
+                         void* stream) {
+  if (B <= 0 || L <= 0) return 0;
+  hipLaunchKernelGGL(segment_info_kernel, dim3((unsigned)((B + 63) / 64)),
+                     dim3(64), 0, static_cast<hipStream_t>(stream), segment_pos,
+                     seg_id, seg_start, (int)B, (int)L);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,252 @@
+/*
+ * cadence_kernels.h -- C ABI of the MI355X (gfx950) CadenceGemma forward path.
+ *
+ * Plain pointers + sizes only (no torch types).  Every entry point:
+ *   - takes device pointers that the caller allocated (no allocation inside),
+ *   - enqueues on `stream` (a hipStream_t passed as void*), never syncs, so
+ *     it is safe to capture into a hipGraph,
+ *   - returns 0 on success or a hipError_t value (hipErrorInvalidValue = 1
+ *     for a shape/alignment contract violation, checked on the host).
+ *
+ * Tensor conventions: bf16 is raw 16-bit storage (uint16_t on the host),
+ * row-major, leading dimensions ("ld*") are in elements.  M = rows (tokens),
+ * N = output features, K = reduction.  Weights W are [N][K] (nn.Linear
+ * layout; weights stored [K][N] by the reference, e.g. Einsum ffw_up, are
+ * packed once by the host).
+ *
+ * The reference (`surakku/cadence-gemma`) has no native layer: each entry
+ * point replaces a sequence of eager PyTorch ops (or timm ops) of the
+ * reference Python path, cited per function.  The Python host
+ * (cadence-gemma_amd/cadence) binds these as torch.ops.cadence.* custom ops.
+ */
+#ifndef CADENCE_KERNELS_H_
+#define CADENCE_KERNELS_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- library info ------------------------------------------------------ */
+
+/* Returns the ABI version (bumped on any signature change). */
+int cadence_abi_version(void);
+
+/* Bytes of fp32 split-K workspace the GEMM entry points need for (M, N, K)
+ * (0 for the tile engine).  `groups` multiplies N for grouped launches. */
+int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
+                                     int64_t groups);
+
+/* ---- GEMMs with fused epilogues ---------------------------------------- */
+
+/* out[map(m), n] = act(A[m,:] . W[n,:] + bias[n]) (+ resid[map(m), n])
+ *   act: 0 = none, 1 = GELU(erf), 3 = GELU(tanh).  map(m) = (m / row_div) * row_mul +
+ *   (m % row_div) + row_off (row_div = M, row_mul = 0, row_off = 0 -> id).
+ * Replaces nn.Linear / F.linear (+ the residual add):
+ *   recurrentgemma/torch/modules.py:634,637,652 (RecurrentBlock linears),
+ *   :429-431,481 (attention projections), :757 (ffw_down), :908,913
+ *   (residual adds); recurrentgemma/projector/mlp.py:13-31 (projector);
+ *   timm ViT qkv / fc1 (+GELU) (dino_siglip.py:85-86 call sites). */
+int cadence_gemm_linear(const void* A, int64_t lda, const void* W, int64_t ldw,
+                        const void* bias, const void* resid, int64_t ld_resid,
+                        void* out, int64_t ldo, int64_t M, int64_t N, int64_t K,
+                        int act, int64_t row_div, int64_t row_mul,
+                        int64_t row_off, void* workspace, int64_t ws_bytes,
+                        void* stream);
+
+/* MLP up-projection + gating: out[m, f] = gelu_tanh(x.Wg[f] + bg[f]) *
+ * (x.Wu[f] + bu[f]).  W is the packed [2F][K] matrix in which every 64-row
+ * group g holds 32 gate rows then the 32 up rows of features
+ * [32g, 32g + 32).  Replaces modules.py:754-756 (Einsum ffw_up + gelu + mul;
+ * layers.py:726-729). */
+int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
+                            const void* bias_gate, const void* bias_up,
+                            void* out, int64_t ldo, int64_t M, int64_t F,
+                            int64_t K, void* workspace, int64_t ws_bytes,
+                            void* stream);
+
+/* RG-LRU gates: both BlockDiagonalLinear layers of one RG-LRU as a grouped
+ * GEMM (one group per head, K = block width) with the full gate chain fused
+ * in the epilogue, producing the scan inputs
+ *   a_out  = reset ? 0 : exp(-8 * sigmoid(gate_a) * softplus(a_param))
+ *   nx_out = x * sigmoid(gate_x) * (reset ? 1 : sqrt(1 - a^2))
+ * with the bf16 rounding chain of the reference.  Wpacked is
+ * [heads][2*bw][bw] (per 64-row group: 32 input-gate rows, 32 a-gate rows).
+ * Replaces layers.py:345-365 (+ 132-142 BlockDiagonalLinear, + 173). */
+int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
+                        const void* bias_x, const void* bias_a,
+                        const void* softplus_a, const int32_t* segment_pos,
+                        void* a_out, void* nx_out, int64_t ldo, int64_t M,
+                        int64_t heads, int64_t bw, void* workspace,
+                        int64_t ws_bytes, void* stream);
+
+/* ViT residual branch (fp32 residual stream, in place):
+ *   resid[m, n] += gamma[n] * (A[m,:] . W[n,:] + bias[n])   (gamma may be 0)
+ * Replaces timm Block `x + ls(attn.proj(.))` / `x + ls(mlp.fc2(.))`. */
+int cadence_gemm_vit_residual(const void* A, int64_t lda, const void* W,
+                              int64_t ldw, const void* bias, const void* gamma,
+                              float* resid, int64_t ld_resid, int64_t M,
+                              int64_t N, int64_t K, void* workspace,
+                              int64_t ws_bytes, void* stream);
+
+/* Patch embedding as GEMM over im2col patches (K padded to 64):
+ *   resid[b, prefix + p, n] = patches[b*P + p, :] . W[n, :] + bias[n] + pos[p, n]
+ * Replaces timm PatchEmbed conv + _pos_embed (no_embed_class). */
+int cadence_gemm_patch_embed(const void* patches, int64_t ldp, const void* W,
+                             int64_t ldw, const void* bias, const void* pos,
+                             float* resid, int64_t B, int64_t P, int64_t ntok,
+                             int64_t prefix, int64_t N, int64_t K,
+                             void* workspace, int64_t ws_bytes, void* stream);
+
+/* Last-position logits with soft-cap and greedy argmax:
+ *   l = bf16(x . E[v]); l = bf16(bf16(tanh(bf16(l / cap))) * cap)
+ *   next[m] = argmax_v l (lowest index on ties); logits_out optional.
+ * Replaces modules.py:1003-1006 + griffin.py:216-221 + the greedy
+ * torch.argmax of examples/cadence_sampler.py:101-110.  `scratch` must hold
+ * M * ceil(V / 64) * 8 bytes plus the split-K workspace. */
+int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
+                          int64_t M, int64_t V, int64_t D, float soft_cap,
+                          void* logits_out, int32_t* next_token,
+                          void* scratch, int64_t scratch_bytes, void* stream);
+int64_t cadence_logits_scratch_bytes(int64_t M, int64_t V, int64_t D);
+
+/* All-position logits (Griffin.forward with return_logits=True,
+ * griffin.py:216-221): out[m, v] = softcap(bf16(x[m] . E[v])) (cap 0 = off).
+ * Uses the GEMM workspace rules of cadence_gemm_linear. */
+int cadence_gemm_logits(const void* X, int64_t ldx, const void* E, int64_t M,
+                        int64_t V, int64_t D, float soft_cap, void* out,
+                        int64_t ldo, void* workspace, int64_t ws_bytes,
+                        void* stream);
+
+/* ---- normalisation / embedding ----------------------------------------- */
+
+/* Griffin RMSNorm, bf16 rounding at every op: layers.py:70-78. */
+int cadence_rmsnorm(const void* x, int64_t ldx, const void* scale, void* out,
+                    int64_t ldo, int64_t rows, int64_t width, float eps,
+                    void* stream);
+
+/* LayerNorm over an fp32 residual stream -> bf16 (timm ViT norm1/norm2,
+ * eps 1e-6). */
+int cadence_layernorm(const float* x, int64_t ldx, const void* weight,
+                      const void* bias, void* out, int64_t ldo, int64_t rows,
+                      int64_t width, float eps, void* stream);
+
+/* Embedder.encode (modules.py:994-1001): out[map(m)] = E[tok[m]] * scale
+ * (scale = bf16(sqrt(width)) or 1), row remap as in cadence_gemm_linear. */
+int cadence_embed(const int32_t* tokens, const void* E, void* out,
+                  int64_t ldo, int64_t M, int64_t D, float scale,
+                  int64_t row_div, int64_t row_mul, int64_t row_off,
+                  void* stream);
+
+/* ---- recurrent block ----------------------------------------------------- */
+
+/* Conv1D, prefill (cache_in == NULL) or single-token decode (L == 1,
+ * cache_in = previous [B,3,E] state).  compat = 1 keeps the reference
+ * document mask (layers.py:629, range(1, shift-1); App. A Q3).  Writes the
+ * new [B, W-1, E] state to cache_out (may alias cache_in only for decode).
+ * Replaces layers.py:457-546 (+ :592-633). */
+int cadence_conv1d(const void* x, int64_t ldx, const void* w, const void* b,
+                   const int32_t* segment_pos, const void* cache_in,
+                   void* out, int64_t ldo, void* cache_out, int64_t B,
+                   int64_t L, int64_t E, int64_t temporal_width, int compat,
+                   void* stream);
+
+/* Linear recurrence h_t = a_t * h_{t-1} + x_t (fp32 state, separate mul and
+ * add as the eager reference), y_t = bf16(h_t), optionally gated:
+ * out_t = bf16(y_t * gate_t) (RecurrentBlock `x * y`, modules.py:651).
+ * `reset` (int32 segment positions, may be NULL) zeroes a where pos == 0.
+ * h0 may be NULL (zeros).  h_last [B,E] fp32.  Replaces layers.py:145-199
+ * (`rnn_scan`) and the join of modules.py:651. */
+int cadence_rnn_scan(const void* x, int64_t ldx, const void* a, int64_t lda,
+                     const int32_t* segment_pos, const float* h0,
+                     const void* gate, int64_t ldg, void* out, int64_t ldo,
+                     float* h_last, int64_t B, int64_t L, int64_t E,
+                     void* stream);
+
+/* ---- local attention ------------------------------------------------------ */
+
+/* Segment bookkeeping for the forward-pass mask (modules.py:130-152):
+ * seg_id = cumsum(pos == 0), seg_start = first index of the row's segment. */
+int cadence_segment_info(const int32_t* segment_pos, int32_t* seg_id,
+                         int32_t* seg_start, int64_t B, int64_t L,
+                         void* stream);
+
+/* RoPE on the first half of each head (modules.py:53-87) for q (H heads)
+ * and k (1 head) read from the fused qkv projection rows; v copied.
+ * q_out [M, H*hd], k_out/v_out [M, hd]. */
+int cadence_rope_qkv(const void* qkv, int64_t ldqkv, const int32_t* positions,
+                     void* q_out, void* k_out, void* v_out, int64_t M,
+                     int64_t H, int64_t hd, void* stream);
+
+/* Prefill local MQA attention, flash-style (modules.py:466-480):
+ * logits = bf16(q.k) * hd^-0.5, mask = same segment & causal & window,
+ * fp32 online softmax, out [B*L, H*hd] bf16. */
+int cadence_local_attention(const void* q, const void* k, const void* v,
+                            const int32_t* seg_id, const int32_t* seg_start,
+                            void* out, int64_t B, int64_t L, int64_t H,
+                            int64_t hd, int64_t window, void* stream);
+
+/* KV cache from the prompt (modules.py:260-290): roll by num_tokens and
+ * right-pad to the window; num_tokens = pos[:, -1] + 1. */
+int cadence_kv_cache_fill(const void* k, const void* v,
+                          const int32_t* segment_pos, void* cache_k,
+                          void* cache_v, int32_t* num_tokens, int64_t B,
+                          int64_t L, int64_t hd, int64_t window, void* stream);
+
+/* Single-token decode attention over the ring buffer + the new key, with the
+ * slot positions of _compute_cache_mask (modules.py:155-185), then the
+ * in-place cache update of _update_attention_cache (modules.py:210-218). */
+int cadence_local_attention_decode(const void* q, const void* k_new,
+                                   const void* v_new, void* cache_k,
+                                   void* cache_v, int32_t* num_tokens,
+                                   void* out, int64_t B, int64_t H,
+                                   int64_t hd, int64_t window, void* stream);
+
+/* ---- vision tower ---------------------------------------------------------- */
+
+/* im2col with the per-encoder Normalize folded in: pixels [B,3,S,S] fp32 in
+ * [0,1] -> patches [B*g*g, Kpad] bf16 (c, kh, kw order, zero padded). */
+int cadence_im2col_normalize(const float* pixels, void* patches, int64_t ldp,
+                             int64_t B, int64_t S, int64_t patch,
+                             const float* mean3, const float* std3,
+                             void* stream);
+
+/* Writes the prefix tokens (cls / register) into rows [0, prefix) of every
+ * image of the fp32 residual stream. */
+int cadence_vit_prefix(const void* tokens, float* resid, int64_t B,
+                       int64_t ntok, int64_t prefix, int64_t D, void* stream);
+
+/* Bidirectional multi-head attention (timm Attention, fused SDPA):
+ * qkv [B*N, 3*H*hd] bf16 -> out [B*N, H*hd] bf16; hd in {64, 72}. */
+int cadence_vit_attention(const void* qkv, void* out, int64_t B, int64_t N,
+                          int64_t H, int64_t hd, void* stream);
+
+/* Drops the prefix tokens and converts the fp32 stream to the bf16
+ * projector input at a column offset: out[b*P + p, col_off + d] =
+ * bf16(resid[b, prefix + p, d])  (dino_siglip.py:153-154 cat + mlp.py:30
+ * `.to(bfloat16)`). */
+int cadence_vit_features(const float* resid, void* out, int64_t ldo,
+                         int64_t col_off, int64_t B, int64_t ntok,
+                         int64_t prefix, int64_t D, void* stream);
+
+/* ---- misc ------------------------------------------------------------------ */
+
+/* Image splice positions (griffin.py:186-191, n_vis generalised):
+ * out[b] = [0, 1, ..., n_vis-1, text_pos[b, :]]. */
+int cadence_splice_positions(const int32_t* text_pos, int32_t* out,
+                             int64_t B, int64_t T, int64_t n_vis,
+                             void* stream);
+
+/* Greedy decode bookkeeping (the host loop of examples/cadence_sampler.py:
+ * 131-151 moved on device): tokens_out[b, *step] = next_token[b];
+ * positions[b] += 1; *step += 1.  B <= 256. */
+int cadence_decode_advance(const int32_t* next_token, int32_t* tokens_out,
+                           int64_t ld_out, int32_t* step, int32_t* positions,
+                           int64_t B, void* stream);
+
+#ifdef __cplusplus
+}  // extern "C"
+#endif
+
+#endif  // CADENCE_KERNELS_H_

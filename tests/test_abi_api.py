@@ -1,0 +1,138 @@
+"""C-ABI library + Python API surface (CPU only; no compute calls)."""
+
+import os
+import re
+
+import pytest
+import torch
+
+import cadence
+from cadence import _lib, common
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "cadence_kernels.h")
+
+
+def declared_symbols():
+  text = open(HEADER).read()
+  text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+  return sorted(set(re.findall(r"\b(cadence_\w+)\s*\(", text)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+  lib = _lib.load()
+  syms = declared_symbols()
+  assert len(syms) >= 25
+  for s in syms:
+    assert hasattr(lib, s), s
+  assert set(syms) == set(_lib.exported_symbols())
+  assert lib.cadence_abi_version() == _lib.ABI_VERSION
+
+
+def test_host_contract_checks_without_gpu():
+  lib = _lib.load()
+  # workspace query is host-only arithmetic
+  assert lib.cadence_gemm_workspace_bytes(4096, 2560, 2560, 1) == 0
+  assert lib.cadence_gemm_workspace_bytes(32, 2560, 2560, 1) > 0
+  # contract violations are rejected before any launch (N % 64 != 0)
+  assert lib.cadence_gemm_linear(None, 0, None, 0, None, None, 0, None, 0, 8,
+                                 100, 64, 0, 8, 0, 0, None, 0, None) != 0
+
+
+def test_reference_exports_present():
+  # recurrentgemma/torch/__init__.py:42-59
+  for name in ("ScanType", "TemporalBlockType", "rnn_scan",
+               "BlockDiagonalLinear", "RGLRU", "Conv1D", "RecurrentBlockCache",
+               "RecurrentBlock", "AttentionBlockCache", "LocalAttentionBlock",
+               "ResidualBlockCache", "ResidualBlock", "Preset",
+               "GriffinConfig", "Griffin", "Sampler"):
+    assert name in cadence.__all__ and hasattr(cadence, name), name
+  assert hasattr(cadence, "VisionEncoder") and hasattr(cadence, "MLPProjector")
+
+
+def test_preset_2b():
+  cfg = common.GriffinConfig.from_preset(common.Preset.RECURRENT_GEMMA_2B_V1)
+  assert (cfg.width, cfg.mlp_expanded_width, cfg.num_heads, cfg.lru_width,
+          cfg.num_layers, cfg.attention_window_size,
+          cfg.logits_soft_cap) == (2560, 7680, 10, 2560, 26, 2048, 30.0)
+  kinds = [k.name[0] for k in cfg.block_types]
+  assert "".join(kinds[:6]) == "RRARRA" and kinds.count("A") == 8
+  assert common.GriffinConfig.from_preset(
+      common.Preset.RECURRENT_GEMMA_2B_V1,
+      max_sequence_length=512).attention_window_size == 512
+
+
+def test_state_dict_keys_and_config_inference_cpu_init():
+  RA = common.TemporalBlockType
+  cfg = common.GriffinConfig(
+      vocab_size=64, width=256, mlp_expanded_width=768, num_heads=4,
+      block_types=(RA.RECURRENT, RA.ATTENTION),
+      embeddings_scale_by_sqrt_dim=True, attention_window_size=64,
+      logits_soft_cap=30.0)
+  vis = common.VisionConfig(
+      image_size=28,
+      dino=common.ViTConfig("dino", 128, 1, 2, 256, class_token=True,
+                            reg_tokens=4, layer_scale=True),
+      siglip=common.ViTConfig("siglip", 128, 1, 2, 200),
+      feature_block=0)
+  m = cadence.Griffin(cfg, dtype=torch.bfloat16, vision=vis)
+  sd = m.state_dict()
+  expected = {
+      "embedder.input_embedding", "final_norm.scale",
+      "blocks.0.temporal_pre_norm.scale", "blocks.0.channel_pre_norm.scale",
+      "blocks.0.recurrent_block.linear_x.weight",
+      "blocks.0.recurrent_block.linear_y.bias",
+      "blocks.0.recurrent_block.linear_out.weight",
+      "blocks.0.recurrent_block.conv_1d.w", "blocks.0.recurrent_block.conv_1d.b",
+      "blocks.0.recurrent_block.rg_lru.a_param",
+      "blocks.0.recurrent_block.rg_lru.input_gate.w",
+      "blocks.0.recurrent_block.rg_lru.a_gate.b",
+      "blocks.0.mlp_block.ffw_up.w", "blocks.0.mlp_block.ffw_up.b",
+      "blocks.0.mlp_block.ffw_down.weight", "blocks.0.mlp_block.ffw_down.bias",
+      "blocks.1.attention_block.proj_q.weight",
+      "blocks.1.attention_block.proj_k.weight",
+      "blocks.1.attention_block.proj_v.weight",
+      "blocks.1.attention_block.proj_final.weight",
+      "blocks.1.attention_block.proj_final.bias",
+      "projector.proj.0.weight", "projector.proj.2.bias",
+      "projector.proj.4.weight",
+      "vis_encoder.dino.patch_embed.proj.weight", "vis_encoder.dino.pos_embed",
+      "vis_encoder.dino.cls_token", "vis_encoder.dino.reg_token",
+      "vis_encoder.dino.blocks.0.norm1.weight",
+      "vis_encoder.dino.blocks.0.attn.qkv.weight",
+      "vis_encoder.dino.blocks.0.ls1.gamma",
+      "vis_encoder.dino.blocks.0.mlp.fc2.bias",
+      "vis_encoder.siglip.blocks.0.attn.proj.weight",
+  }
+  missing = expected - set(sd)
+  assert not missing, missing
+  assert sd["blocks.0.recurrent_block.rg_lru.a_gate.w"].shape == (4, 64, 64)
+  assert sd["blocks.1.attention_block.proj_k.weight"].shape == (64, 256)
+  assert sd["blocks.0.mlp_block.ffw_up.b"].shape == (2, 1, 1, 768)
+  re_cfg = common.GriffinConfig.from_torch_params(
+      sd, embeddings_scale_by_sqrt_dim=True, attention_window_size=64,
+      logits_soft_cap=30.0)
+  assert re_cfg.block_types == cfg.block_types
+  assert re_cfg.num_heads == 4 and re_cfg.lru_width == 256
+  with pytest.raises(ValueError):
+    common.GriffinConfig.from_torch_params(
+        sd, preset=common.Preset.RECURRENT_GEMMA_2B_V1)
+
+
+def test_rg_lru_init_ring():
+  """rnn_param_init: a = exp(-softplus(param)) lies in [0.9, 0.999]."""
+  lru = cadence.RGLRU(512, 4)
+  a = torch.exp(-torch.nn.functional.softplus(lru.a_param.detach()))
+  assert a.min() >= 0.9 - 1e-4 and a.max() <= 0.999 + 1e-4
+
+
+def test_ops_have_no_cpu_fallback():
+  x = torch.zeros(4, 8, dtype=torch.bfloat16)
+  with pytest.raises((NotImplementedError, RuntimeError)):
+    torch.ops.cadence.rmsnorm(x, torch.zeros(8, dtype=torch.bfloat16), 1e-6)
+
+
+def test_positions_and_sampler_prompt_layout():
+  from cadence.sampler import prompt_positions
+  pos = prompt_positions(torch.tensor([3, 5]), 5)
+  assert pos.tolist() == [[-1, -1, 0, 1, 2], [0, 1, 2, 3, 4]]

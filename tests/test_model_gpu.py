@@ -1,0 +1,220 @@
+"""Model-level parity: cadence.Griffin / Sampler on the GPU vs the oracle.
+
+Mirrors the reference's model tests: `griffin_test.py` (R+A stack, forward
+with two-document positions), `sampler_test.py` (MockVocab, output shapes,
+prefill-vs-sampler forward equivalence at bf16 rtol 1e-4 / atol 1e-2), and
+adds the multimodal splice (`griffin.py:176-191`) with a reduced-depth
+vision tower.
+"""
+
+import pytest
+import torch
+
+from conftest import assert_close_bf16, cosine, rel_l2
+from oracle import griffin_ref as R
+
+import cadence
+from cadence import common
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+RA = common.TemporalBlockType
+
+
+class MockVocab:
+  """Same vocabulary contract as recurrentgemma/torch/sampler_test.py:26-65."""
+  _ids = {"<pad>": 0, "<s>": 1, "</s>": 2, "input": 3, "string": 4,
+          "hello": 5, "world": 6, "Hello": 7, "!": 8, "How": 9, "are": 10,
+          "you?": 11}
+
+  def pad_id(self):
+    return 0
+
+  def bos_id(self):
+    return 1
+
+  def eos_id(self):
+    return 2
+
+  def GetPieceSize(self):
+    return len(self._ids)
+
+  def DecodeIds(self, ids):
+    rev = {v: k for k, v in self._ids.items()}
+    return " ".join(rev.get(i, "?") for i in ids)
+
+  def EncodeAsIds(self, text):
+    return [self._ids[w] for w in text.split(" ")]
+
+
+def small_config(vocab=1024, window=2048, layers=(RA.RECURRENT, RA.ATTENTION,
+                                                   RA.RECURRENT)):
+  return common.GriffinConfig(
+      vocab_size=vocab, width=256, mlp_expanded_width=768, num_heads=4,
+      block_types=tuple(layers), embeddings_scale_by_sqrt_dim=True,
+      attention_window_size=window, logits_soft_cap=30.0)
+
+
+def make_model(dev, cfg, seed=0, vision=None, perturb=True):
+  torch.manual_seed(seed)
+  m = cadence.Griffin(cfg, device=dev, dtype=BF, vision=vision)
+  if perturb:   # avoid all-zero norms / biases so every path is exercised
+    g = torch.Generator(device=dev).manual_seed(seed + 1)
+    with torch.no_grad():
+      for name, p in m.named_parameters():
+        if name.endswith((".scale", ".bias", ".b")) and "vis_encoder" not in name:
+          p.copy_((torch.randn(p.shape, generator=g, device=dev) * 0.1).to(p.dtype))
+  p = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+  return m, p
+
+
+def test_state_dict_keys_match_reference_layout(dev):
+  cfg = small_config()
+  m, p = make_model(dev, cfg, perturb=False)
+  assert p["blocks.0.mlp_block.ffw_up.w"].shape == (2, 256, 768)
+  assert p["blocks.0.mlp_block.ffw_up.b"].shape == (2, 1, 1, 768)
+  assert p["blocks.1.attention_block.proj_k.weight"].shape == (64, 256)
+  assert p["blocks.0.recurrent_block.rg_lru.a_gate.w"].shape == (4, 64, 64)
+  re = common.GriffinConfig.from_torch_params(p)
+  assert re.block_types == cfg.block_types and re.num_heads == 4
+
+
+@pytest.mark.parametrize("window", [2048, 16])
+def test_griffin_forward_two_docs(dev, window):
+  cfg = small_config(window=window)
+  m, p = make_model(dev, cfg)
+  b, t = 2, 64
+  g = torch.Generator().manual_seed(3)
+  tok = torch.randint(3, cfg.vocab_size, (b, t), generator=g, dtype=torch.int32)
+  pos = torch.cat([torch.arange(t // 2), torch.arange(t // 2)]).to(
+      torch.int32)[None].repeat(b, 1)
+  want, _ = R.griffin_forward(p, cfg, tok.long(), pos)
+  got, cache = m(tok.to(dev), pos.to(dev))
+  assert got.shape == (b, t, cfg.vocab_size)
+  assert cosine(got, want) > 0.999, cosine(got, want)
+  assert rel_l2(got, want) < 3e-2
+  assert set(cache) == {"blocks.0", "blocks.1", "blocks.2"}
+
+
+def test_prefill_then_decode_matches_oracle(dev):
+  cfg = small_config(window=32)
+  m, p = make_model(dev, cfg, seed=4)
+  b, t, steps = 3, 40, 12
+  g = torch.Generator().manual_seed(5)
+  tok = torch.randint(3, cfg.vocab_size, (b, t), generator=g, dtype=torch.int32)
+  want_tok, want_logits = R.greedy_sample(p, cfg, tok.long(), steps)
+  vocab = MockVocab()
+  s = cadence.Sampler(m, vocab, use_graph=False)
+  st = s.generate(tok, torch.full((b,), t, dtype=torch.int32), steps,
+                  return_logits=True)
+  got_logits = st.logits_buffer.cpu()
+  # first token comes from identical-state logits: must agree
+  assert torch.equal(st.tokens_buffer[:, 0].cpu().long(), want_tok[:, 0])
+  assert cosine(got_logits[:, 0], want_logits[:, 0]) > 0.999
+  # teacher-forced comparison is not possible through the sampler; report
+  # agreement of the greedy continuation (exact match expected mostly)
+  agree = (st.tokens_buffer.cpu().long() == want_tok).float().mean().item()
+  assert agree >= 0.75, agree
+
+
+def test_decode_graph_matches_eager(dev):
+  cfg = small_config(window=32)
+  m, _ = make_model(dev, cfg, seed=6)
+  vocab = MockVocab()
+  b, t, steps = 4, 20, 16
+  tok = torch.randint(3, cfg.vocab_size, (b, t), dtype=torch.int32)
+  lens = torch.full((b,), t, dtype=torch.int32)
+  eager = cadence.Sampler(m, vocab, use_graph=False).generate(tok, lens, steps)
+  graph = cadence.Sampler(m, vocab, use_graph=True).generate(tok, lens, steps)
+  assert torch.equal(eager.tokens_buffer.cpu(), graph.tokens_buffer.cpu())
+
+
+@pytest.mark.parametrize("echo", [True, False])
+@pytest.mark.parametrize("return_logits", [True, False])
+def test_sampler_output_shapes(dev, echo, return_logits):
+  """sampler_test.py:97-148 with the MI355X kernel constraints on width."""
+  vocab = MockVocab()
+  cfg = small_config(vocab=64)
+  m, _ = make_model(dev, cfg, seed=7)
+  s = cadence.Sampler(m, vocab)
+  raw = "Hello ! How are you?"
+  n_in = 1 + len(raw.split(" "))
+  out = s([raw], total_generation_steps=10, echo=echo,
+          return_logits=return_logits)
+  total = 10 + (n_in if echo else 0)
+  if return_logits:
+    assert len(out.logits) == 1 and out.logits[0].shape == (total, 64)
+  else:
+    assert out.logits == []
+  assert len(out.tokens) == 1 and out.tokens[0].shape == (total,)
+  assert isinstance(out.text[0], str)
+
+
+def test_forward_equivalence(dev):
+  """sampler_test.py:150-230: prompt logits from Griffin.forward equal the
+  sampler's echo logits (bf16 rtol 1e-4, atol 1e-2)."""
+  vocab = MockVocab()
+  cfg = small_config(vocab=64)
+  m, _ = make_model(dev, cfg, seed=8)
+  raw = "Hello ! How are you?"
+  ids = torch.tensor([[1] + vocab.EncodeAsIds(raw)], dtype=torch.int32)
+  n = ids.shape[1]
+  pos = torch.arange(n, dtype=torch.int32)[None]
+  fwd, _ = m(ids.to(dev), pos.to(dev))
+  out = cadence.Sampler(m, vocab)([raw], 10, echo=True, return_logits=True)
+  # positions 0..n-2 come from the prefill forward (same kernels), the last
+  # prompt position from the cached step
+  torch.testing.assert_close(fwd[0, :n - 1].float().cpu(),
+                             out.logits[0][:n - 1].float().cpu(),
+                             rtol=1e-4, atol=1e-2)
+
+
+def tiny_vision(image_size=56):
+  dino = common.ViTConfig(name="dino", width=1024, depth=2, num_heads=16,
+                          mlp_width=4096, class_token=True, reg_tokens=4,
+                          layer_scale=True)
+  sig = common.ViTConfig(name="siglip", width=1152, depth=2, num_heads=16,
+                         mlp_width=4304, mean=common.SIGLIP_MEAN,
+                         std=common.SIGLIP_STD)
+  return common.VisionConfig(image_size=image_size, dino=dino, siglip=sig,
+                             feature_block=1)
+
+
+def test_vision_and_projector_vs_oracle(dev):
+  vis = tiny_vision()
+  cfg = small_config()
+  m, p = make_model(dev, cfg, seed=9, vision=vis)
+  with torch.no_grad():   # make LayerScale matter
+    for blk in list(m.vis_encoder.dino.blocks):
+      blk.ls1.gamma.fill_(0.5)
+      blk.ls2.gamma.fill_(0.5)
+  p = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+  g = torch.Generator().manual_seed(10)
+  px = torch.rand(2, 3, 56, 56, generator=g)
+  want = R.vision_encoder(px, p, vis)
+  got = m.vis_encoder.encode(px.to(dev))
+  assert got.shape == (2, 16, 2176)
+  assert rel_l2(got, want) < 1e-2, rel_l2(got, want)
+  want_tok = R.projector(want, p)
+  got_tok = m.projector(got)
+  assert rel_l2(got_tok, want_tok) < 2e-2
+
+
+def test_multimodal_prefill_vs_oracle(dev):
+  vis = tiny_vision()
+  cfg = small_config()
+  m, p = make_model(dev, cfg, seed=11, vision=vis)
+  g = torch.Generator().manual_seed(12)
+  b, t = 2, 12
+  px = torch.rand(b, 3, 56, 56, generator=g)
+  tok = torch.randint(3, cfg.vocab_size, (b, t), generator=g, dtype=torch.int32)
+  tok[:, 0] = 2
+  pos = torch.arange(t, dtype=torch.int32)[None].repeat(b, 1)
+  img = R.image_tokens(px, p, vis)
+  want, _ = R.griffin_forward(p, cfg, tok.long(), pos, image_tokens=img)
+  got, _ = m(tok.to(dev), pos.to(dev), images=px.to(dev))
+  assert got.shape == (b, 16 + t, cfg.vocab_size)
+  assert cosine(got, want) > 0.999, cosine(got, want)
+  # no image when the positions hold no 0 (decode): plain text forward
+  got2, _ = m(tok[:, 3:].to(dev), pos[:, 3:].to(dev), images=px.to(dev))
+  assert got2.shape == (b, t - 3, cfg.vocab_size)
