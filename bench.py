@@ -1,0 +1,245 @@
+#!/usr/bin/env python
+"""CadenceGemma multimodal prefill+decode benchmark on MI355X.
+
+Metric (BASELINE.json): multimodal prefill+decode tokens/sec, Cadence-2B,
+224 px, bs=32 per GPU, 1 -> 8 MI355X.  One step = one batch through the
+whole hot path: dual ViT (DINOv2-L/14-reg4 + SigLIP-so400m/14, 23 blocks
+each) -> projector -> Griffin-2B prefill on [image | prompt[:-1]] -> cached
+step on the last prompt token -> 31 greedy decode steps (hipGraph replay)
+-> one all-gather of the generated tokens (RCCL on N > 1).
+Tokens per step per GPU = B * (n_vis + prompt + decode) = 32 * (256+64+32).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
+
+Prints ONE JSON line on rank 0 (see the driver contract in the task).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "cadence-gemma_amd"), ROOT):
+  if _p not in sys.path:
+    sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+import cadence  # noqa: E402
+from cadence import common, distributed as D, ops  # noqa: E402
+
+METRIC = ("multimodal prefill+decode tokens/sec, Cadence-2B 224px bs=32, "
+          "1→8 MI355X")
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_BF16_PEAK_TFS = 2500.0    # dense bf16 MFMA spec
+
+
+class BenchVocab:
+  """Synthetic token ids only; the Gemma tokenizer is not shipped."""
+
+  def pad_id(self):
+    return 0
+
+  def bos_id(self):
+    return 2
+
+  def eos_id(self):
+    return 1
+
+
+def parse():
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--gpus", type=int, default=1)
+  ap.add_argument("--steps", type=int, default=5)
+  ap.add_argument("--warmup", type=int, default=2)
+  ap.add_argument("--batch", type=int, default=32, help="samples per GPU")
+  ap.add_argument("--image-size", type=int, default=224)
+  ap.add_argument("--prompt", type=int, default=64)
+  ap.add_argument("--decode", type=int, default=32)
+  ap.add_argument("--no-cpu-baseline", action="store_true")
+  ap.add_argument("--cpu-decode-steps", type=int, default=32)
+  ap.add_argument("--no-kernel-timing", action="store_true")
+  ap.add_argument("--text-only", action="store_true",
+                  help="C2-style text-only run (no vision tower)")
+  return ap.parse_args()
+
+
+def build_model(dev, image_size, text_only):
+  torch.manual_seed(0)
+  cfg = common.GriffinConfig.from_preset(common.Preset.RECURRENT_GEMMA_2B_V1)
+  vis = None if text_only else common.VisionConfig(image_size=image_size)
+  with torch.no_grad():
+    model = cadence.Griffin(cfg, device=dev, dtype=torch.bfloat16, vision=vis)
+  model.eval()
+  return cfg, vis, model
+
+
+def make_inputs(global_batch, lo, hi, image_size, prompt, vocab, text_only):
+  g = torch.Generator().manual_seed(4321)
+  tok = torch.randint(3, vocab, (global_batch, prompt), generator=g,
+                      dtype=torch.int32)
+  tok[:, 0] = BenchVocab().bos_id()
+  images = None
+  if not text_only:
+    gi = torch.Generator().manual_seed(1234)
+    # generated per-rank slice of the same global stream (no 8x host copy)
+    per = hi - lo
+    gi.manual_seed(1234 + lo)
+    images = torch.rand(per, 3, image_size, image_size, generator=gi)
+  return tok[lo:hi].contiguous(), images
+
+
+def roofline_entry(summary, key, bound):
+  s = summary.get(key)
+  if not s or s["avg_ms"] <= 0:
+    return None
+  if bound == "hbm":
+    achieved = s["avg_work"] / (s["avg_ms"] * 1e-3) / 1e9
+    peak, unit = HBM_PEAK_GBS, "GB/s"
+  else:
+    achieved = s["avg_work"] / (s["avg_ms"] * 1e-3) / 1e12
+    peak, unit = MFMA_BF16_PEAK_TFS, "TFLOP/s"
+  return {"kernel": key, "bound": bound, "achieved": round(achieved, 2),
+          "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
+          "traffic": None, "avg_us": round(s["avg_ms"] * 1e3, 2),
+          "launches": s["launches"],
+          "work_per_launch": s["avg_work"]}
+
+
+def cpu_baseline(model, cfg, vis, tokens, images, decode_steps):
+  """The oracle (reference op sequence, B = 1 like the reference) on host
+  cores, on a bounded sample: 1 sample, full image + prompt prefill,
+  `decode_steps` greedy decode steps."""
+  from oracle import griffin_ref as R
+  cores = min(len(os.sched_getaffinity(0)), int(os.environ.get(
+      "OMP_NUM_THREADS", "16") or 16))
+  torch.set_num_threads(cores)
+  p = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+  tok = tokens[:1].cpu().long()
+  px = None if images is None else images[:1].cpu()
+  t0 = time.perf_counter()
+  R.greedy_sample(p, cfg, tok, decode_steps, pixels=px, vcfg=vis)
+  dt = time.perf_counter() - t0
+  n_vis = 0 if vis is None else vis.n_visual_tokens
+  ntok = n_vis + tok.shape[1] + decode_steps
+  return {"value": round(ntok / dt, 2), "unit": "tokens/s", "cores": cores,
+          "kind": "port",
+          "sample": (f"1 sample (B=1, the reference cannot batch): "
+                     f"{n_vis} image + {tok.shape[1]} prompt tokens prefill + "
+                     f"{decode_steps} decode steps, {dt:.1f} s"),
+          "seconds": round(dt, 2)}
+
+
+def main():
+  args = parse()
+  rank, world, local = D.init_from_env()
+  if world != args.gpus and rank == 0:
+    print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+  dev = torch.device("cuda", local)
+  torch.cuda.set_device(dev)
+  cfg, vis, model = build_model(dev, args.image_size, args.text_only)
+  n_vis = 0 if vis is None else vis.n_visual_tokens
+  gb = args.batch * world
+  lo, hi = D.shard_range(gb, rank, world)
+  tok_cpu, img_cpu = make_inputs(gb, lo, hi, args.image_size, args.prompt,
+                                 cfg.vocab_size, args.text_only)
+  tokens = tok_cpu.to(dev)
+  images = None if img_cpu is None else img_cpu.to(dev)
+  lengths = torch.full((args.batch,), args.prompt, dtype=torch.int32)
+  sampler = cadence.Sampler(model, BenchVocab(), use_graph=True)
+
+  def step(events=None):
+    st = sampler.generate(tokens, lengths, args.decode, images=images,
+                          events=events)
+    return D.gather_rows(st.tokens_buffer)
+
+  with torch.no_grad():
+    for _ in range(args.warmup):
+      out = step()
+    torch.cuda.synchronize()
+    D.barrier()
+    ops.TIMER.reset()
+    ops.TIMER.enabled = not args.no_kernel_timing
+    prefill_ms = []
+    ev_list = []
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+      ev = {}
+      out = step(ev)
+      ev_list.append(ev)
+    torch.cuda.synchronize()
+    D.barrier()
+    t1 = time.perf_counter()
+    ops.TIMER.enabled = False
+  elapsed = D.max_over_ranks(t1 - t0)
+  for ev in ev_list:
+    prefill_ms.append(ev["prefill_start"].elapsed_time(ev["prefill_end"]))
+  ksum = ops.TIMER.summary() if not args.no_kernel_timing else {}
+
+  tok_per_step = gb * (n_vis + args.prompt + args.decode)
+  value = tok_per_step * args.steps / elapsed
+  ms_step = elapsed / args.steps * 1e3
+  pre_ms = sum(prefill_ms) / max(len(prefill_ms), 1)
+  pre_ms = D.max_over_ranks(pre_ms)
+  prefill_tps = gb * (n_vis + args.prompt - 1) / (pre_ms * 1e-3)
+
+  result = None
+  if rank == 0:
+    gemm_keys = [k for k in ksum if k.startswith("gemm_tile_kernel")]
+    dom = max(gemm_keys, key=lambda k: ksum[k]["total_ms"]) if gemm_keys else None
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": ("synthetic: torch.rand images (seed 1234), random prompt "
+                 "tokens (seed 4321), random-init weights (seed 0)"),
+        "config": {
+            "workload": ("Cadence-2B (RecurrentGemma-2B + DINOv2-L/14-reg4 + "
+                         "SigLIP-so400m/14 + MLP projector) "
+                         + ("text-only" if args.text_only else
+                            f"{args.image_size}px") +
+                         f", bs={args.batch}/GPU, prompt {args.prompt}, "
+                         f"greedy decode {args.decode}"),
+            "global_batch": gb, "image_size": None if args.text_only
+            else args.image_size, "n_visual_tokens": n_vis,
+            "prompt_len": args.prompt, "decode_steps": args.decode,
+            "seq_len": n_vis + args.prompt + args.decode,
+            "parallelism": f"dp{world}",
+        },
+        "prefill_ms": round(pre_ms, 3),
+        "prefill_tokens_per_s": round(prefill_tps, 1),
+        "roofline": roofline_entry(ksum, dom, "mfma") if dom else None,
+        "roofline_scan": roofline_entry(ksum, "rnn_scan_kernel", "hbm"),
+        "kernels": {k: {"launches": v["launches"],
+                        "avg_us": round(v["avg_ms"] * 1e3, 2),
+                        "total_ms_per_step": round(v["total_ms"] / args.steps, 3)}
+                    for k, v in sorted(ksum.items())},
+        "generated_tokens_checksum": int(out.long().sum().item()),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+      result["cpu_baseline"] = cpu_baseline(model, cfg, vis, tok_cpu, img_cpu,
+                                            args.cpu_decode_steps)
+    else:
+      result["cpu_baseline"] = None
+    print(json.dumps(result), flush=True)
+  D.barrier()
+  D.shutdown()
+
+
+if __name__ == "__main__":
+  main()

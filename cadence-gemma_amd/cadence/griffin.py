@@ -1,4 +1,5 @@
-"""CadenceGemma model assembly on MI355X.
+"""CadenceGemma model assembly on MI355X (inference only: no backward kernels,
+so the entry points run under torch.no_grad()).
 
 Reference: `recurrentgemma/torch/griffin.py` (`Griffin` :35-245).  Same
 constructor / `forward(tokens, segment_pos, cache, return_logits,
@@ -73,11 +74,11 @@ class Griffin(nn.Module):
     return 0 if self.vision_config is None else self.vision_config.n_visual_tokens
 
   def _pixels(self, images, img_path, batch: int):
+    dev = self.embedder.input_embedding.device
     if images is not None:
-      return images.to(torch.float32).contiguous()
+      return images.to(dev, torch.float32).contiguous()
     from . import image_io
     px = image_io.load_image(img_path, self.vision_config.image_size)
-    dev = self.embedder.input_embedding.device
     return px[None].expand(batch, -1, -1, -1).contiguous().to(dev)
 
   def embed_inputs(self, tokens, segment_pos, images=None, img_path=None):
@@ -116,6 +117,7 @@ class Griffin(nn.Module):
 
   # ------------------------------------------------------------------ API
 
+  @torch.no_grad()
   def forward(self, tokens: torch.Tensor, segment_pos: torch.Tensor,
               cache: Cache | None = None, return_logits: bool = True,
               return_cache: bool = True, img_path: str | None = None,
@@ -138,6 +140,7 @@ class Griffin(nn.Module):
                                  float(self.config.logits_soft_cap or 0.0))
     return logits.view(b, length, -1), new_cache
 
+  @torch.no_grad()
   def next_token(self, tokens: torch.Tensor, segment_pos: torch.Tensor,
                  cache: Cache, return_logits: bool = False,
                  inplace: bool = True):

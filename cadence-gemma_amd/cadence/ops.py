@@ -55,6 +55,56 @@ def _mat(t: torch.Tensor, name: str, dtype=_BF16) -> int:
   return t.stride(0)
 
 
+class KernelTimer:
+  """HIP-event timing of selected kernels on the stream they run on.
+
+  Off by default.  When enabled (bench.py), each timed op brackets its
+  launch(es) with two events on the current stream and records the
+  algorithmic work of that launch; `summary()` syncs and returns per-kernel
+  launch counts, average duration and average work.  Never records while a
+  graph is being captured.
+  """
+
+  def __init__(self):
+    self.enabled = False
+    self.records: dict[str, list] = {}
+
+  def reset(self):
+    self.records = {}
+
+  def start(self, t: torch.Tensor):
+    if not self.enabled or torch.cuda.is_current_stream_capturing():
+      return None
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record(torch.cuda.current_stream(t.device))
+    return ev
+
+  def stop(self, ev, key: str, work: float, t: torch.Tensor):
+    if ev is None:
+      return
+    end = torch.cuda.Event(enable_timing=True)
+    end.record(torch.cuda.current_stream(t.device))
+    self.records.setdefault(key, []).append((ev, end, float(work)))
+
+  def summary(self) -> dict[str, dict]:
+    torch.cuda.synchronize()
+    out = {}
+    for key, recs in self.records.items():
+      ms = [a.elapsed_time(b) for a, b, _ in recs]
+      work = [w for _, _, w in recs]
+      out[key] = dict(launches=len(recs), total_ms=sum(ms),
+                      avg_ms=sum(ms) / len(ms), avg_work=sum(work) / len(work),
+                      total_work=sum(work))
+    return out
+
+
+TIMER = KernelTimer()
+
+
+def _tile(M: int) -> bool:
+  return M > 64
+
+
 def _ws(M: int, N: int, K: int, groups: int, like: torch.Tensor):
   n = _lib.load().cadence_gemm_workspace_bytes(M, N, K, groups)
   if n == 0:
@@ -77,9 +127,11 @@ def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off):
   if bias is not None:
     _need(bias.numel() == N and bias.dtype == _BF16, "bias shape/dtype")
   ws, nws = _ws(M, N, K, 1, a)
+  ev = TIMER.start(a) if _tile(M) else None
   _lib.check(_lib.load().cadence_gemm_linear(
       _p(a), lda, _p(w), ldw, _p(bias), _p(resid), ldr, _p(out), ldo, M, N, K,
       act, row_div, row_mul, row_off, _p(ws), nws, _s(a)), "gemm_linear")
+  TIMER.stop(ev, "gemm_tile_kernel<EpiLinear>", 2.0 * M * N * K, a)
 
 
 @_reg("gated_gelu(Tensor a, Tensor w_packed, Tensor bias_gate, "
@@ -91,9 +143,11 @@ def _gated_gelu(a, w_packed, bias_gate, bias_up):
   _need(w_packed.shape[1] == K and w_packed.is_contiguous(), "w_packed")
   out = torch.empty(M, F, dtype=_BF16, device=a.device)
   ws, nws = _ws(M, 2 * F, K, 1, a)
+  ev = TIMER.start(a) if _tile(M) else None
   _lib.check(_lib.load().cadence_gemm_gated_gelu(
       _p(a), lda, _p(w_packed), _p(bias_gate), _p(bias_up), _p(out), F, M, F,
       K, _p(ws), nws, _s(a)), "gated_gelu")
+  TIMER.stop(ev, "gemm_tile_kernel<EpiGatedGelu>", 4.0 * M * F * K, a)
   return out
 
 
@@ -108,10 +162,12 @@ def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos):
   a = torch.empty(M, E, dtype=_BF16, device=x.device)
   nx = torch.empty(M, E, dtype=_BF16, device=x.device)
   ws, nws = _ws(M, 2 * bw, bw, H, x)
+  ev = TIMER.start(x) if _tile(M) else None
   _lib.check(_lib.load().cadence_rglru_gates(
       _p(x), ldx, _p(w_packed), _p(bias_x), _p(bias_a), _p(softplus_a),
       _p(segment_pos.contiguous()), _p(a), _p(nx), E, M, H, bw, _p(ws), nws,
       _s(x)), "rglru_gates")
+  TIMER.stop(ev, "gemm_tile_kernel<EpiRglruGates>", 2.0 * M * 2 * bw * bw * H, x)
   return a, nx
 
 
@@ -123,9 +179,11 @@ def _vit_residual(a, w, bias, gamma, resid):
   M, K = a.shape
   N = w.shape[0]
   ws, nws = _ws(M, N, K, 1, a)
+  ev = TIMER.start(a) if _tile(M) else None
   _lib.check(_lib.load().cadence_gemm_vit_residual(
       _p(a), lda, _p(w), ldw, _p(bias), _p(gamma), _p(resid), ldr, M, N, K,
       _p(ws), nws, _s(a)), "vit_residual")
+  TIMER.stop(ev, "gemm_tile_kernel<EpiVitResid>", 2.0 * M * N * K, a)
 
 
 @_reg("patch_embed_(Tensor patches, Tensor w, Tensor bias, Tensor pos, "
@@ -235,9 +293,16 @@ def _rnn_scan(x, a, segment_pos, h0, gate, B, L):
   out = torch.empty(B * L, E, dtype=_BF16, device=x.device)
   h_last = torch.empty(B, E, dtype=_F32, device=x.device)
   pos = segment_pos.contiguous() if segment_pos is not None else None
+  ev = TIMER.start(x) if L > 1 else None
   _lib.check(_lib.load().cadence_rnn_scan(
       _p(x), ldx, _p(a), lda, _p(pos), _p(h0), _p(gate), ldg, _p(out), E,
       _p(h_last), B, L, E, _s(x)), "rnn_scan")
+  # algorithmic bytes: x, a (+ gate) in and y out as bf16 per element,
+  # fp32 state out (+ in), int32 reset per token when given
+  per_elem = 6 + (2 if gate is not None else 0)
+  nbytes = (B * L * E * per_elem + B * E * 4 * (2 if h0 is not None else 1)
+            + (B * L * 4 if pos is not None else 0))
+  TIMER.stop(ev, "rnn_scan_kernel", nbytes, x)
   return out, h_last
 
 
@@ -274,9 +339,11 @@ def _local_attention(q, k, v, seg_id, seg_start, B, L, H, hd, window):
   for t in (q, k, v):
     _need(t.is_contiguous() and t.dtype == _BF16, "q/k/v contiguous bf16")
   out = torch.empty(B * L, H * hd, dtype=_BF16, device=q.device)
+  ev = TIMER.start(q)
   _lib.check(_lib.load().cadence_local_attention(
       _p(q), _p(k), _p(v), _p(seg_id), _p(seg_start), _p(out), B, L, H, hd,
       window, _s(q)), "local_attention")
+  TIMER.stop(ev, "flash_attn_kernel<local>", 4.0 * B * H * L * L * hd / 2, q)
   return out
 
 
@@ -343,8 +410,11 @@ def _vit_prefix(tokens, resid, B, ntok, prefix):
 def _vit_attention(qkv, B, N, H, hd):
   _need(qkv.is_contiguous() and qkv.dtype == _BF16, "qkv contiguous bf16")
   out = torch.empty(B * N, H * hd, dtype=_BF16, device=qkv.device)
+  ev = TIMER.start(qkv)
   _lib.check(_lib.load().cadence_vit_attention(
       _p(qkv), _p(out), B, N, H, hd, _s(qkv)), "vit_attention")
+  TIMER.stop(ev, f"flash_attn_kernel<vit,hd{hd}>", 4.0 * B * H * N * N * hd,
+             qkv)
   return out
 
 

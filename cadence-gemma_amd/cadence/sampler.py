@@ -102,8 +102,13 @@ class Sampler:
   def generate(self, tokens: torch.Tensor, input_lengths: torch.Tensor,
                total_generation_steps: int, images=None, img_path=None,
                return_logits: bool = False, echo: bool = False,
-               end_sampling_at_eos_token: bool = False) -> SamplingState:
-    """Prefill + decode for a left-padded [B, T] prompt batch (on device)."""
+               end_sampling_at_eos_token: bool = False,
+               events: dict | None = None) -> SamplingState:
+    """Prefill + decode for a left-padded [B, T] prompt batch (on device).
+
+    `events`, if given, receives HIP events bracketing the prefill
+    ("prefill_start"/"prefill_end") on the current stream.
+    """
     dev = self.device
     b, t = tokens.shape
     positions = prompt_positions(input_lengths.cpu(), t).to(dev)
@@ -119,10 +124,16 @@ class Sampler:
                            None, torch.zeros(b, dtype=torch.bool), lb)
     model = self.model
     prev_logits = None
+    if events is not None:
+      events["prefill_start"] = torch.cuda.Event(enable_timing=True)
+      events["prefill_end"] = torch.cuda.Event(enable_timing=True)
+      events["prefill_start"].record()
     if t > 1:
       prev_logits, cache = self.apply_model(tokens[:, :-1], positions[:, :-1],
                                             None, return_logits and echo, True,
                                             img_path, images)
+      if events is not None:
+        events["prefill_end"].record()
       nxt, logits, cache = model.next_token(tokens[:, -1:], positions[:, -1:],
                                             cache, return_logits)
     else:
@@ -184,28 +195,17 @@ class Sampler:
     return bool((buf == self.vocab.eos_id()).any(dim=1).all())
 
   def _decode_graph(self, cur, pos, cache, buf, step, n_more, eos_stop):
-    """Captures one in-place decode step into a hipGraph and replays it."""
-    model = self.model
-    stream = torch.cuda.Stream(device=cur.device)
-    stream.wait_stream(torch.cuda.current_stream(cur.device))
-
-    def one_step():
-      nxt, _, _ = model.next_token(cur[:, None], pos[:, None], cache, False,
-                                   inplace=True)
-      ops.ops.decode_advance_(nxt, buf, step, pos)
-      cur.copy_(nxt)
-
-    with torch.cuda.stream(stream):
-      one_step()                      # step 1 eagerly (also warms the pools)
-      graph = torch.cuda.CUDAGraph()
-      with torch.cuda.graph(graph, stream=stream):
-        one_step()
-      # the capture recorded but did not execute step 2: replay covers it
-      for i in range(n_more - 1):
-        graph.replay()
-        if eos_stop and (i % 8 == 7) and self._all_done(buf):
-          break
-    torch.cuda.current_stream(cur.device).wait_stream(stream)
+    """Replays a captured single-token decode step `n_more` times."""
+    key = (cur.shape[0], cur.device)
+    eng = self._graphs.get(key) if hasattr(self, "_graphs") else None
+    if eng is None or eng.max_steps < buf.shape[1]:
+      if not hasattr(self, "_graphs"):
+        self._graphs = {}
+      eng = _DecodeGraph(self.model, cache, cur.shape[0], buf.shape[1],
+                         cur.device)
+      self._graphs[key] = eng
+    eng.run(cache, cur, pos, buf, step, n_more,
+            (lambda b: self._all_done(b)) if eos_stop else None)
 
   # ------------------------------------------------------------------- API
 
@@ -233,3 +233,65 @@ class Sampler:
     return SamplerOutput(
         text=[self.vocab.DecodeIds(t.tolist()) for t in toks],
         logits=logits, tokens=toks)
+
+
+def _clone_cache(cache):
+  return {k: type(v)(*[t.clone() for t in v]) for k, v in cache.items()}
+
+
+class _DecodeGraph:
+  """One single-token decode step captured into a hipGraph.
+
+  Static buffers: current token, positions, token buffer, step counter and a
+  private copy of every block cache (recurrent states and attention ring
+  buffers are updated in place by the kernels).  `run` copies the prefill
+  state in, replays the graph, and copies the generated tokens out.
+  """
+
+  def __init__(self, model, cache_like, batch, max_steps, device):
+    self.model = model
+    self.max_steps = max_steps
+    self.cur = torch.zeros(batch, dtype=torch.int32, device=device)
+    self.pos = torch.zeros(batch, dtype=torch.int32, device=device)
+    self.buf = torch.zeros(batch, max_steps, dtype=torch.int32, device=device)
+    self.step = torch.ones(1, dtype=torch.int32, device=device)
+    self.cache = _clone_cache(cache_like)
+    self.stream = torch.cuda.Stream(device=device)
+    self.stream.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(self.stream):
+      self._step()                     # warm-up (allocator pools, packing)
+      self.graph = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(self.graph, stream=self.stream):
+        self._step()
+    torch.cuda.current_stream(device).wait_stream(self.stream)
+
+  def _step(self):
+    nxt, _, _ = self.model.next_token(self.cur[:, None], self.pos[:, None],
+                                      self.cache, False, inplace=True)
+    ops.ops.decode_advance_(nxt, self.buf, self.step, self.pos)
+    self.cur.copy_(nxt)
+
+  def run(self, cache, cur, pos, buf, step, n_more, all_done=None):
+    dev_stream = torch.cuda.current_stream(cur.device)
+    for name, c in cache.items():
+      for dst, src in zip(self.cache[name], c):
+        dst.copy_(src)
+    self.cur.copy_(cur)
+    self.pos.copy_(pos)
+    self.step.fill_(1)
+    self.stream.wait_stream(dev_stream)
+    with torch.cuda.stream(self.stream):
+      for i in range(n_more):
+        self.graph.replay()
+        if all_done is not None and (i % 8 == 7) and all_done(
+            self.buf[:, :buf.shape[1]]):
+          break
+    dev_stream.wait_stream(self.stream)
+    steps = buf.shape[1]
+    buf[:, 1:].copy_(self.buf[:, 1:steps])
+    step.copy_(self.step)
+    pos.copy_(self.pos)
+    cur.copy_(self.cur)
+    for name, c in cache.items():
+      for dst, src in zip(c, self.cache[name]):
+        dst.copy_(src)
