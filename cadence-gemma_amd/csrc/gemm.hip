@@ -254,6 +254,142 @@ __global__ __launch_bounds__(256, 2) void gemm_tile_kernel(
   }
 }
 
+// ------------------------------------------------- big tile engine (DMA)
+//
+// 256x256x64 block tile, 8 waves (2 M x 4 N), wave tile 128x64 =
+// 8x4 mfma_f32_16x16x32_bf16.  Operands go HBM -> LDS by LDS-DMA
+// (global_load_lds_dwordx4: one wave instruction = 1 KiB = 8 rows of 128 B,
+// no VGPR staging, no ds_write), two LDS buffers (128 KiB), one barrier
+// per K tile.  The XOR chunk swizzle is applied on the per-lane SOURCE
+// address (LDS image stays lane-linear) and again on the ds_read address
+// (it is an involution), which keeps the 16-lane ds_read_b128 groups
+// conflict-free.  Rows past M / N are clamped on load and masked at the
+// store, so any M and any N % 64 == 0 work.
+
+typedef const void __attribute__((address_space(1)))* gptr_t;
+typedef void __attribute__((address_space(3)))* lptr_t;
+
+template <class Epi>
+__global__ __launch_bounds__(512, 1) void gemm_big_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
+    int64_t ldw, int M, int N, int K, int64_t a_goff, int64_t w_goff,
+    Epi epi) {
+  constexpr int BM = 256, BN = 256, MR = 8, NR = 4;
+  constexpr int ROWS = BM + BN;               // LDS rows per buffer (128 B)
+  __shared__ __attribute__((aligned(16))) uint4 smem[2 * ROWS * 8];
+
+  const int g = blockIdx.y;
+  A += g * a_goff;
+  W += g * w_goff;
+
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN, nt = ntm * ntn;
+  int t = blockIdx.x;
+  {
+    const int xcd = t & 7, q = nt >> 3, r = nt & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    t = base + (t >> 3);
+  }
+  constexpr int GM = 4;
+  const int grp = t / (GM * ntn), fm = grp * GM;
+  const int gs = min(ntm - fm, GM);
+  const int within = t % (GM * ntn);
+  const int tm = fm + within % gs, tn = within / gs;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // DMA mapping: wave w moves pieces 8w..8w+7 of the 64 pieces of a K tile
+  // (pieces 0..31 = A rows, 32..63 = W rows); lane l of a piece lands at LDS
+  // row 8*piece + l/8, slot l%8, so it loads source chunk (l%8) ^ (l/8).
+  const int src_chunk = (lane & 7) ^ (lane >> 3);
+  const u16* src[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int piece = wave * 8 + i;
+    if (piece < 32) {
+      const int r = min(m0 + piece * 8 + (lane >> 3), M - 1);
+      src[i] = A + (int64_t)r * lda + src_chunk * 8;
+    } else {
+      const int r = min(n0 + (piece - 32) * 8 + (lane >> 3), N - 1);
+      src[i] = W + (int64_t)r * ldw + src_chunk * 8;
+    }
+  }
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int piece = wave * 8 + i;
+      __builtin_amdgcn_global_load_lds(
+          (gptr_t)(src[i] + k0),
+          (lptr_t)(&smem[(buf * ROWS + piece * 8) * 8]), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  const int sw = lane & 7;  // (row & 7) of every row this lane reads
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+    const uint4* As = &smem[cur * ROWS * 8];
+    const uint4* Bs = &smem[(cur * ROWS + BM) * 8];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = (s * 4 + (lane >> 4)) ^ sw;
+      bf16x8 bfr[NR];
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        bfr[j] = __builtin_bit_cast(
+            bf16x8, Bs[(wn * 64 + j * 16 + (lane & 15)) * 8 + ch]);
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        const bf16x8 af = __builtin_bit_cast(
+            bf16x8, As[(wm * 128 + i * 16 + (lane & 15)) * 8 + ch]);
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j],
+                                                              acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // waits this wave's DMA (vmcnt) + all waves' reads
+  }
+
+  const int mbase = m0 + wm * 128, nbase = n0 + wn * 64;
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+  if constexpr (Epi::kPaired) {
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mbase + i * 16 + rsub + r;
+          if (row < M && nbase < N)
+            epi.apply2(row, nbase / 2 + j * 16 + csub, acc[i][j][r],
+                       acc[i][j + 2][r], g);
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mbase + i * 16 + rsub + r;
+          const int col = nbase + j * 16 + csub;
+          if (row < M && col < N) epi.apply(row, col, acc[i][j][r], g);
+        }
+  }
+}
+
 // ---------------------------------------------------------- skinny engine
 
 // One block: 64 output columns x MS rows over one K split; 4 waves split the
@@ -430,6 +566,13 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(
 
 constexpr int kSkinnyMaxM = 64;
 
+// CADENCE_GEMM_LEGACY=1 selects the 128x128 register-staged tile kernel
+// (A/B comparisons in one binary).
+bool use_legacy_tile() {
+  const char* e = getenv("CADENCE_GEMM_LEGACY");
+  return e && e[0] == '1';
+}
+
 int skinny_splits(int64_t N, int64_t K, int64_t groups) {
   const int64_t tiles = (N / 64) * groups;
   const int64_t ksteps = K / 32;
@@ -454,11 +597,19 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                 hipStream_t st) {
   if (M <= 0) return 0;
   if (M > kSkinnyMaxM) {
-    if (N % 128 || K % BK) return (int)hipErrorInvalidValue;
-    const int64_t tiles = ((M + 127) / 128) * (N / 128);
+    if (N % 64 || K % BK) return (int)hipErrorInvalidValue;
+    if (use_legacy_tile() && N % 128 == 0) {
+      const int64_t tiles = ((M + 127) / 128) * (N / 128);
+      dim3 grid((unsigned)tiles, (unsigned)groups);
+      hipLaunchKernelGGL((gemm_tile_kernel<128, 128, Epi>), grid, dim3(256), 0, st,
+                         A, lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff,
+                         epi);
+      return (int)hipGetLastError();
+    }
+    const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
     dim3 grid((unsigned)tiles, (unsigned)groups);
-    hipLaunchKernelGGL((gemm_tile_kernel<128, 128, Epi>), grid, dim3(256), 0, st,
-                       A, lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
+    hipLaunchKernelGGL((gemm_big_kernel<Epi>), grid, dim3(512), 0, st, A, lda, W,
+                       ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
     return (int)hipGetLastError();
   }
   if (N % 64 || K % 32) return (int)hipErrorInvalidValue;
