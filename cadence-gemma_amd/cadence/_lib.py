@@ -51,7 +51,8 @@ _SIGS: dict[str, list] = {
     "cadence_rnn_scan": [P, I64, P, I64, P, P, P, I64, P, I64, P, I64, I64, I64,
                          P],
     "cadence_segment_info": [P, P, P, I64, I64, P],
-    "cadence_rope_qkv": [P, I64, P, P, P, P, I64, I64, I64, P],
+    "cadence_rope_qkv": [P, I64, P, P, P, P, I64, I64, I64, P, I64, P],
+    "cadence_rope_table": [P, I64, I64, P],
     "cadence_local_attention": [P, P, P, P, P, P, I64, I64, I64, I64, I64, P],
     "cadence_kv_cache_fill": [P, P, P, P, P, P, I64, I64, I64, I64, P],
     "cadence_local_attention_decode": [P, P, P, P, P, P, P, I64, I64, I64, I64,

@@ -94,7 +94,8 @@ class LocalAttentionBlock(nn.Module):
     """Attention branch on normalised rows; returns (resid + out, cache)."""
     h, hd = self.num_heads, self.head_dim
     qkv = ops.linear(xn2d, self.qkv_weight())
-    q, k, v = ops.ops.rope_qkv(qkv, pos.view(-1), h, hd)
+    q, k, v = ops.ops.rope_qkv(qkv, pos.view(-1), h, hd,
+                               ops.rope_table(qkv.device, hd))
     if cache is None:
       seg, start = ops.ops.segment_info(pos)
       enc = ops.ops.local_attention(q, k, v, seg, start, b, t, h, hd,
@@ -186,6 +187,17 @@ class RecurrentBlock(nn.Module):
     w, bias = self.yx_weight()
     yx = ops.linear(xn2d, w, bias)                       # [M, 2E]: y | x
     y_br, x_br = yx[:, :e], yx[:, e:]
+    if (inplace_state and return_cache and cache is not None and t == 1 and
+        cache.conv1d_state.is_contiguous() and
+        cache.conv1d_state.dtype == xn2d.dtype):
+      # decode: conv / RG-LRU states are advanced in place by the kernels
+      conv_out = ops.ops.conv1d_step_(x_br, self.conv_1d.w, self.conv_1d.b,
+                                      cache.conv1d_state)
+      a, nx = self.rg_lru.gates(conv_out, pos.view(-1))
+      gated = ops.ops.rnn_scan_(nx, a, cache.rg_lru_state, y_br, b, t)
+      out = ops.linear(gated, self.linear_out.weight, self.linear_out.bias,
+                       resid=resid2d)
+      return out, cache
     conv_out, conv_state = self.conv_1d.apply2d(
         x_br, pos, None if cache is None else cache.conv1d_state, b, t)
     a, nx = self.rg_lru.gates(conv_out, pos.view(-1))

@@ -306,6 +306,36 @@ def _rnn_scan(x, a, segment_pos, h0, gate, B, L):
   return out, h_last
 
 
+@_reg("conv1d_step_(Tensor x, Tensor w, Tensor b, Tensor(a!) state) -> Tensor")
+def _conv1d_step(x, w, b, state):
+  """Single-token Conv1D updating its [B, W-1, E] state in place."""
+  ldx = _mat(x, "x")
+  B, E = x.shape
+  TW = w.shape[0]
+  _need(state.is_contiguous() and state.dtype == _BF16 and
+        tuple(state.shape) == (B, TW - 1, E), "conv state")
+  out = torch.empty(B, E, dtype=_BF16, device=x.device)
+  _lib.check(_lib.load().cadence_conv1d(
+      _p(x), ldx, _p(w), _p(b), None, _p(state), _p(out), E, _p(state), B, 1,
+      E, TW, 1, _s(x)), "conv1d_step")
+  return out
+
+
+@_reg("rnn_scan_(Tensor x, Tensor a, Tensor(a!) h, Tensor? gate, int B, "
+      "int L) -> Tensor")
+def _rnn_scan_inplace(x, a, h, gate, B, L):
+  """Scan continuing from and updating the fp32 state `h` [B, E] in place."""
+  ldx, lda = _mat(x, "x"), _mat(a, "a")
+  E = x.shape[1]
+  ldg = _mat(gate, "gate") if gate is not None else 0
+  _need(h.dtype == _F32 and h.is_contiguous(), "h fp32")
+  out = torch.empty(B * L, E, dtype=_BF16, device=x.device)
+  _lib.check(_lib.load().cadence_rnn_scan(
+      _p(x), ldx, _p(a), lda, None, _p(h), _p(gate), ldg, _p(out), E, _p(h), B,
+      L, E, _s(x)), "rnn_scan_")
+  return out
+
+
 # ---------------------------------------------------------------- attention
 
 @_reg("segment_info(Tensor segment_pos) -> (Tensor, Tensor)")
@@ -319,17 +349,36 @@ def _segment_info(segment_pos):
   return seg, start
 
 
-@_reg("rope_qkv(Tensor qkv, Tensor positions, int H, int hd) -> "
-      "(Tensor, Tensor, Tensor)")
-def _rope_qkv(qkv, positions, H, hd):
+ROPE_TABLE_POSITIONS = 8192
+_rope_tables: dict = {}
+
+
+def rope_table(device: torch.device, hd: int) -> torch.Tensor:
+  """Per-(device, head dim) bf16 sin/cos table for positions < 8192, built
+  once by a kernel (never reallocated, so captured graphs stay valid)."""
+  key = (str(device), hd)
+  t = _rope_tables.get(key)
+  if t is None:
+    t = torch.empty(ROPE_TABLE_POSITIONS, 2, hd // 4, dtype=_BF16,
+                    device=device)
+    _lib.check(_lib.load().cadence_rope_table(
+        _p(t), ROPE_TABLE_POSITIONS, hd, _s(t)), "rope_table")
+    _rope_tables[key] = t
+  return t
+
+
+@_reg("rope_qkv(Tensor qkv, Tensor positions, int H, int hd, "
+      "Tensor? table=None) -> (Tensor, Tensor, Tensor)")
+def _rope_qkv(qkv, positions, H, hd, table=None):
   ld = _mat(qkv, "qkv")
   M = qkv.shape[0]
   q = torch.empty(M, H * hd, dtype=_BF16, device=qkv.device)
   k = torch.empty(M, hd, dtype=_BF16, device=qkv.device)
   v = torch.empty(M, hd, dtype=_BF16, device=qkv.device)
+  tlen = table.shape[0] if table is not None else 0
   _lib.check(_lib.load().cadence_rope_qkv(
       _p(qkv), ld, _p(positions.contiguous()), _p(q), _p(k), _p(v), M, H, hd,
-      _s(qkv)), "rope_qkv")
+      _p(table), tlen, _s(qkv)), "rope_qkv")
   return q, k, v
 
 

@@ -239,14 +239,19 @@ struct DecodeArgs {
   float scale;
 };
 
+// 4 waves per sequence: all stage the K / V^T tiles, each computes the
+// (cheap) 16 x 32 score tile and softmax redundantly, and each owns a
+// quarter of the head dim in P.V and in the output.
 template <int HD>
-__global__ __launch_bounds__(64) void decode_attn_kernel(DecodeArgs a) {
-  constexpr int KS = HD / 32, NO = HD / 16, CPR = HD / 8;
+__global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
+  constexpr int KS = HD / 32, NO = HD / 16 / 4, CPR = HD / 8;
   __shared__ uint4 ks_[KT * HD / 8];
   __shared__ u16 vt[HD * KT];
-  __shared__ u16 pt[16 * KT];
+  __shared__ u16 ptall[4][16 * KT];
   const int b = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  u16* pt = ptall[wave];
+  const int dbase = wave * NO * 16;
   const int nt = a.num_tokens[b];
   const int qpos = nt;
   const int kblk = nt / a.W;
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeArgs a) {
   for (int k0 = 0; k0 < nslots; k0 += KT) {
     if (k0 >= slot_hi && k0 + KT <= a.W) continue;  // no valid slot in tile
     __syncthreads();
-    for (int c = lane; c < KT * CPR; c += 64) {
+    for (int c = tid; c < KT * CPR; c += 256) {
       const int kr = c / CPR, ch = c % CPR;
       const int slot = k0 + kr;
       const int d = ch * 8;
@@ -362,14 +367,15 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         pt[(4 * (lane >> 4) + r) * KT + jn * 16 + (lane & 15)] = f2bf(p[jn][r]);
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
     const bf16x8 pf = __builtin_bit_cast(
         bf16x8, *reinterpret_cast<const uint4*>(pt + (lane & 15) * KT + 8 * (lane >> 4)));
 #pragma unroll
     for (int j = 0; j < NO; ++j) {
       const bf16x8 vf = __builtin_bit_cast(
-          bf16x8, *reinterpret_cast<const uint4*>(&vt[(j * 16 + (lane & 15)) * KT +
-                                                     8 * (lane >> 4)]));
+          bf16x8, *reinterpret_cast<const uint4*>(
+                      &vt[(dbase + j * 16 + (lane & 15)) * KT + 8 * (lane >> 4)]));
       o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[j], 0, 0, 0);
     }
   }
@@ -380,7 +386,7 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeArgs a) {
     const float inv = l_run[r] > 0.0f ? 1.0f / l_run[r] : 0.0f;
 #pragma unroll
     for (int j = 0; j < NO; ++j) {
-      const int d = j * 16 + (lane & 15);
+      const int d = dbase + j * 16 + (lane & 15);
       a.o[(int64_t)b * a.H * a.hd + hrow * a.hd + d] = f2bf(o[j][r] * inv);
     }
   }
@@ -388,13 +394,13 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeArgs a) {
   // bump num_tokens (all reads of this sequence's cache are done).
   __syncthreads();
   const int slot = nt % a.W;
-  for (int d = lane * 8; d < a.hd; d += 512) {
+  for (int d = tid * 8; d < a.hd; d += 2048) {
     st16(a.ck + ((int64_t)b * a.W + slot) * a.hd + d,
          ld16(a.k_new + (int64_t)b * a.new_rs + d));
     st16(a.cv + ((int64_t)b * a.W + slot) * a.hd + d,
          ld16(a.v_new + (int64_t)b * a.new_rs + d));
   }
-  if (lane == 0) a.num_tokens[b] = nt + 1;
+  if (tid == 0) a.num_tokens[b] = nt + 1;
 }
 
 // ------------------------------------------------------------------- RoPE
@@ -402,10 +408,34 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeArgs a) {
 // One thread: 8 rotation pairs (16-B loads) of one head of one row, plus
 // the matching 16 pass-through dims.  Heads 0..H-1 are queries, head H is
 // the key; v is copied by head H's threads.
+// modules.py:73-81: fp32 inverse frequency (10000 ** (2i / rope_dim))^-1,
+// fp32 angle pos * inv, sin / cos rounded to the activation dtype.
+CADENCE_DEV void rope_sincos(int pos, int fi, int half, float& sn, float& cs) {
+  const float expo = (float)(2 * fi) / (float)half;
+  const float timescale = (float)pow(10000.0, (double)expo);
+  const float inv = 1.0f / timescale;
+  const float ang = (float)pos * inv;
+  sn = rbf((float)sin((double)ang));
+  cs = rbf((float)cos((double)ang));
+}
+
+__global__ __launch_bounds__(256) void rope_table_kernel(u16* __restrict__ t,
+                                                         int P, int hd) {
+  const int quarter = hd / 4, half = hd / 2;
+  for (int64_t idx = blockIdx.x * 256 + threadIdx.x; idx < (int64_t)P * quarter;
+       idx += (int64_t)gridDim.x * 256) {
+    const int p = idx / quarter, i = idx % quarter;
+    float sn, cs;
+    rope_sincos(p, i, half, sn, cs);
+    t[((int64_t)p * 2) * quarter + i] = f2bf(sn);
+    t[((int64_t)p * 2 + 1) * quarter + i] = f2bf(cs);
+  }
+}
+
 __global__ __launch_bounds__(256) void rope_qkv_kernel(
     const u16* __restrict__ qkv, int64_t ld, const int32_t* __restrict__ pos,
     u16* __restrict__ qo, u16* __restrict__ ko, u16* __restrict__ vo, int64_t M,
-    int H, int hd) {
+    int H, int hd, const u16* __restrict__ table, int table_len) {
   const int half = hd / 2, quarter = hd / 4;  // rope dims, pairs
   const int cpq = quarter / 8;                // threads per head
   const int64_t total = M * (H + 1) * cpq;
@@ -421,19 +451,20 @@ __global__ __launch_bounds__(256) void rope_qkv_kernel(
     float x1[8], x2[8];
     unpack8(ld16(src + i0), x1);
     unpack8(ld16(src + quarter + i0), x2);
-    const float p = (float)pos[m];
+    const int p = pos[m];
+    float sn[8], cs[8];
+    if (p >= 0 && p < table_len) {
+      unpack8(ld16(table + ((int64_t)p * 2) * quarter + i0), sn);
+      unpack8(ld16(table + ((int64_t)p * 2 + 1) * quarter + i0), cs);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rope_sincos(p, i0 + i, half, sn[i], cs[i]);
+    }
     float o1[8], o2[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int fi = i0 + i;
-      const float expo = (float)(2 * fi) / (float)half;
-      const float timescale = (float)pow(10000.0, (double)expo);
-      const float inv = 1.0f / timescale;
-      const float ang = p * inv;
-      const float sn = rbf((float)sin((double)ang));
-      const float cs = rbf((float)cos((double)ang));
-      o1[i] = bsub(bmul(x1[i], cs), bmul(x2[i], sn));
-      o2[i] = badd(bmul(x2[i], cs), bmul(x1[i], sn));
+      o1[i] = bsub(bmul(x1[i], cs[i]), bmul(x2[i], sn[i]));
+      o2[i] = badd(bmul(x2[i], cs[i]), bmul(x1[i], sn[i]));
     }
     st16(dst + i0, pack8(o1));
     st16(dst + quarter + i0, pack8(o2));
@@ -498,7 +529,8 @@ extern "C" {
 
 int cadence_rope_qkv(const void* qkv, int64_t ldqkv, const int32_t* positions,
                      void* q_out, void* k_out, void* v_out, int64_t M,
-                     int64_t H, int64_t hd, void* stream) {
+                     int64_t H, int64_t hd, const void* table,
+                     int64_t table_len, void* stream) {
   if (hd % 64 || ldqkv % 8) return (int)hipErrorInvalidValue;
   if (M <= 0) return 0;
   const int cpq = (int)(hd / 4 / 8);
@@ -506,7 +538,17 @@ int cadence_rope_qkv(const void* qkv, int64_t ldqkv, const int32_t* positions,
                      0, static_cast<hipStream_t>(stream),
                      static_cast<const u16*>(qkv), ldqkv, positions,
                      static_cast<u16*>(q_out), static_cast<u16*>(k_out),
-                     static_cast<u16*>(v_out), M, (int)H, (int)hd);
+                     static_cast<u16*>(v_out), M, (int)H, (int)hd,
+                     static_cast<const u16*>(table), table ? (int)table_len : 0);
+  return (int)hipGetLastError();
+}
+
+int cadence_rope_table(void* table, int64_t positions, int64_t hd,
+                       void* stream) {
+  if (hd % 64 || positions <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(rope_table_kernel, dim3(grid_cap(positions * (hd / 4))),
+                     dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<u16*>(table), (int)positions, (int)hd);
   return (int)hipGetLastError();
 }
 
@@ -580,11 +622,11 @@ int cadence_local_attention_decode(const void* q, const void* k_new,
                (int)window, 1.0f / sqrtf((float)hd)};
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (hd == 256)
-    hipLaunchKernelGGL(decode_attn_kernel<256>, dim3((unsigned)B), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(decode_attn_kernel<256>, dim3((unsigned)B), dim3(256), 0, st, a);
   else if (hd == 128)
-    hipLaunchKernelGGL(decode_attn_kernel<128>, dim3((unsigned)B), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(decode_attn_kernel<128>, dim3((unsigned)B), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(decode_attn_kernel<64>, dim3((unsigned)B), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(decode_attn_kernel<64>, dim3((unsigned)B), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -20,6 +20,7 @@
 //  EpiRglruGates  RG-LRU gate chain -> (a, normalized_x)       layers.py:345-365
 //  EpiVitResid    timm residual: resid += gamma * (x.W + b)   (fp32 stream)
 //  EpiPatch       patch-embed conv as GEMM + pos_embed at a prefix offset
+#include <cstring>
 #include "common.hpp"
 #include "../../include/cadence_kernels.h"
 
@@ -390,6 +391,268 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
   }
 }
 
+// ---------------------------------------------------------- decode engine
+//
+// M <= 64 rows (decode batch).  One workgroup = 16 output columns (paired
+// epilogues: the 16 gate + 16 up packed columns of 16 outputs), 8 waves
+// stride over K in 32-deep steps, each weight byte is read exactly once
+// straight into MFMA B fragments (no LDS staging), A (the activations,
+// L2-resident) likewise.  Partial accumulators are summed through LDS in a
+// fixed wave order (deterministic) and the epilogue is applied in the same
+// kernel: no split-K slabs, no reduce launch.
+
+template <int MS, class Epi>
+__global__ __launch_bounds__(512) void gemm_decode_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
+    int64_t ldw, int M, int N, int K, int64_t a_goff, int64_t w_goff,
+    Epi epi) {
+  constexpr int MR = MS / 16;
+  constexpr int NREP = Epi::kPaired ? 2 : 1;
+  constexpr int U = 4;
+  __shared__ float red[8][MS * 16 * NREP];
+  const int g = blockIdx.y;
+  A += g * a_goff;
+  W += g * w_goff;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int col[NREP];
+  if constexpr (Epi::kPaired) {
+    const int grp = blockIdx.x >> 1, half = blockIdx.x & 1;
+    col[0] = grp * 64 + half * 16;
+    col[NREP - 1] = grp * 64 + 32 + half * 16;
+  } else {
+    col[0] = blockIdx.x * 16;
+  }
+  const int koff = 8 * (lane >> 4);
+  const int ksteps = K / 32;
+  f32x4 acc[MR][NREP];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  const u16* wrow[NREP];
+#pragma unroll
+  for (int j = 0; j < NREP; ++j)
+    wrow[j] = W + (int64_t)(col[j] + (lane & 15)) * ldw + koff;
+  for (int ks0 = wave; ks0 < ksteps; ks0 += 8 * U) {
+    uint4 wb[U][NREP], xa[U][MR];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ks = ks0 + 8 * u;
+      const bool ok = ks < ksteps;
+      const int k = ks * 32;
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) wb[u][j] = ok ? ld16(wrow[j] + k) : zero;
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        const int m = i * 16 + (lane & 15);
+        xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + k + koff) : zero;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NREP; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, xa[u][i]),
+              __builtin_bit_cast(bf16x8, wb[u][j]), acc[i][j], 0, 0, 0);
+  }
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[wave][((i * 16 + rsub + r) * NREP + j) * 16 + csub] = acc[i][j][r];
+  __syncthreads();
+  for (int o = threadIdx.x; o < MS * 16; o += 512) {
+    const int m = o / 16, c = o % 16;
+    if (m >= M) continue;
+    float v[NREP];
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      const int idx = (m * NREP + j) * 16 + c;
+      v[j] = ((red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx])) +
+             ((red[4][idx] + red[5][idx]) + (red[6][idx] + red[7][idx]));
+    }
+    if constexpr (Epi::kPaired) {
+      const int grp = blockIdx.x >> 1, half = blockIdx.x & 1;
+      epi.apply2(m, grp * 32 + half * 16 + c, v[0], v[NREP - 1], g);
+    } else {
+      if (col[0] + c < N) epi.apply(m, col[0] + c, v[0], g);
+    }
+  }
+}
+
+// Weight-streaming decode GEMM (M <= 32).  One workgroup = 16 output columns
+// (paired: 16 gate + 16 up packed columns) x one K split; wave w owns k-steps
+// w, w+8, ..., at most KSW of them, and issues ALL of its weight and
+// activation loads before the first MFMA, so a workgroup waits for HBM once.
+// parts == nullptr: fixed-order LDS reduction + fused epilogue.  Otherwise
+// raw fp32 partials go to parts[split][M][N] for splitk_reduce_kernel.
+template <int MS, int KSW, class Epi>
+__global__ __launch_bounds__(512) void gemm_stream_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
+    int64_t ldw, int M, int N, int K, int klen, int64_t a_goff, int64_t w_goff,
+    float* __restrict__ parts, Epi epi) {
+  constexpr int MR = MS / 16;
+  constexpr int NREP = Epi::kPaired ? 2 : 1;
+  __shared__ float red[8][MS * 16 * NREP];
+  const int g = blockIdx.z;
+  A += g * a_goff;
+  W += g * w_goff;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int col[NREP];
+  if constexpr (Epi::kPaired) {
+    const int grp = blockIdx.x >> 1, half = blockIdx.x & 1;
+    col[0] = grp * 64 + half * 16;
+    col[NREP - 1] = grp * 64 + 32 + half * 16;
+  } else {
+    col[0] = blockIdx.x * 16;
+  }
+  const int koff = 8 * (lane >> 4);
+  const int kbeg = blockIdx.y * klen;
+  const int kend = min(K, kbeg + klen);
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  uint4 wb[KSW][NREP], xa[KSW][MR];
+#pragma unroll
+  for (int u = 0; u < KSW; ++u) {
+    const int k = kbeg + (wave + 8 * u) * 32;
+    const bool ok = k < kend;
+#pragma unroll
+    for (int j = 0; j < NREP; ++j)
+      wb[u][j] = ok ? ld16(W + (int64_t)(col[j] + (lane & 15)) * ldw + k + koff)
+                    : zero;
+  }
+#pragma unroll
+  for (int u = 0; u < KSW; ++u) {
+    const int k = kbeg + (wave + 8 * u) * 32;
+    const bool ok = k < kend;
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int m = i * 16 + (lane & 15);
+      xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + k + koff) : zero;
+    }
+  }
+  f32x4 acc[MR][NREP];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < KSW; ++u)
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NREP; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8, xa[u][i]),
+            __builtin_bit_cast(bf16x8, wb[u][j]), acc[i][j], 0, 0, 0);
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[wave][((i * 16 + rsub + r) * NREP + j) * 16 + csub] = acc[i][j][r];
+  __syncthreads();
+  for (int o = threadIdx.x; o < MS * 16; o += 512) {
+    const int m = o / 16, c = o % 16;
+    if (m >= M) continue;
+    float v[NREP];
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      const int idx = (m * NREP + j) * 16 + c;
+      v[j] = ((red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx])) +
+             ((red[4][idx] + red[5][idx]) + (red[6][idx] + red[7][idx]));
+    }
+    if (parts) {
+      float* dst = parts + ((int64_t)blockIdx.y * gridDim.z + g) * (int64_t)M * N +
+                   (int64_t)m * N;
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) dst[col[j] + c] = v[j];
+    } else if constexpr (Epi::kPaired) {
+      const int grp = blockIdx.x >> 1, half = blockIdx.x & 1;
+      epi.apply2(m, grp * 32 + half * 16 + c, v[0], v[NREP - 1], g);
+    } else {
+      epi.apply(m, col[0] + c, v[0], g);
+    }
+  }
+}
+
+// Logits: the decode engine's main loop + soft-cap + per-workgroup argmax.
+template <int MS>
+__global__ __launch_bounds__(512) void logits_decode_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
+    int64_t ldw, int M, int V, int K, float cap, u16* __restrict__ logits,
+    float* __restrict__ bval, int* __restrict__ bidx) {
+  constexpr int MR = MS / 16;
+  constexpr int U = 4;
+  __shared__ float red[8][MS * 16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16;
+  const int koff = 8 * (lane >> 4);
+  const int ksteps = K / 32;
+  f32x4 acc[MR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  const u16* wrow = W + (int64_t)(n0 + (lane & 15)) * ldw + koff;
+  for (int ks0 = wave; ks0 < ksteps; ks0 += 8 * U) {
+    uint4 wb[U], xa[U][MR];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ks = ks0 + 8 * u;
+      const bool ok = ks < ksteps;
+      wb[u] = ok ? ld16(wrow + ks * 32) : zero;
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        const int m = i * 16 + (lane & 15);
+        xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + ks * 32 + koff) : zero;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8, xa[u][i]), __builtin_bit_cast(bf16x8, wb[u]),
+            acc[i], 0, 0, 0);
+  }
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][(i * 16 + rsub + r) * 16 + csub] = acc[i][r];
+  __syncthreads();
+  // thread o -> (row m, column c); 16 consecutive threads share a row
+  for (int o = threadIdx.x; o < MS * 16; o += 512) {
+    const int m = o / 16, c = o % 16;
+    float v = ((red[0][o] + red[1][o]) + (red[2][o] + red[3][o])) +
+              ((red[4][o] + red[5][o]) + (red[6][o] + red[7][o]));
+    float l = rbf(v);
+    if (cap > 0.0f) l = softcap(l, cap);
+    int idx = n0 + c;
+    const bool valid = m < M && idx < V;
+    if (valid && logits) logits[(int64_t)m * V + idx] = f2bf(l);
+    if (!valid) { l = -INFINITY; idx = 0x7fffffff; }
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      const float ov = __shfl_xor(l, off, 64);
+      const int oi = __shfl_xor(idx, off, 64);
+      if (ov > l || (ov == l && oi < idx)) { l = ov; idx = oi; }
+    }
+    if (c == 0 && m < M) {
+      bval[(int64_t)m * gridDim.x + blockIdx.x] = l;
+      bidx[(int64_t)m * gridDim.x + blockIdx.x] = idx;
+    }
+  }
+}
+
 // ---------------------------------------------------------- skinny engine
 
 // One block: 64 output columns x MS rows over one K split; 4 waves split the
@@ -568,6 +831,29 @@ constexpr int kSkinnyMaxM = 64;
 
 // CADENCE_GEMM_LEGACY=1 selects the 128x128 register-staged tile kernel
 // (A/B comparisons in one binary).
+// Decode GEMM engine: split-K + ordered reduce (default, measured faster on
+// MI355X at B=32) or CADENCE_DECODE_ENGINE=fused for the single-pass
+// in-kernel-reduction engine.
+bool use_splitk_skinny() {
+  const char* e = getenv("CADENCE_DECODE_ENGINE");
+  return !(e && strncmp(e, "fused", 5) == 0);
+}
+
+// Weight-streaming plan for M <= 32 (CADENCE_DECODE_ENGINE=splitk disables):
+// k-steps per wave (KSW) and K splits so that one split is <= 8 * KSW steps.
+int stream_plan(int64_t M, int64_t K, int* ksw, int* splits) {
+  const char* e = getenv("CADENCE_DECODE_ENGINE");
+  if (M > 32 || K % 32 ||
+      (e && (strncmp(e, "splitk", 6) == 0 || strncmp(e, "fused", 5) == 0)))
+    return 0;
+  const int64_t ks = K / 32;
+  if (ks <= 8) { *ksw = 1; *splits = 1; }
+  else if (ks <= 16) { *ksw = 2; *splits = 1; }
+  else if (ks <= 32) { *ksw = 4; *splits = 1; }
+  else { *ksw = 10; *splits = (int)((ks + 79) / 80); }
+  return 1;
+}
+
 bool use_legacy_tile() {
   const char* e = getenv("CADENCE_GEMM_LEGACY");
   return e && e[0] == '1';
@@ -613,6 +899,58 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
     return (int)hipGetLastError();
   }
   if (N % 64 || K % 32) return (int)hipErrorInvalidValue;
+  int ksw = 0, ssplits = 0;
+  if (stream_plan(M, K, &ksw, &ssplits)) {
+    const unsigned nblk = (unsigned)(Epi::kPaired ? N / 32 : N / 16);
+    const int64_t ks = K / 32;
+    const int klen = (int)((ks + ssplits - 1) / ssplits) * 32;
+    float* parts = nullptr;
+    if (ssplits > 1) {
+      const int64_t need = (int64_t)ssplits * groups * M * N * 4;
+      if (!ws || ws_bytes < need) return (int)hipErrorInvalidValue;
+      parts = static_cast<float*>(ws);
+    }
+    dim3 grid(nblk, (unsigned)ssplits, (unsigned)groups);
+#define CADENCE_STREAM(MS_, KSW_)                                               \
+  hipLaunchKernelGGL((gemm_stream_kernel<MS_, KSW_, Epi>), grid, dim3(512), 0, st, \
+                     A, lda, W, ldw, (int)M, (int)N, (int)K, klen, a_goff,      \
+                     w_goff, parts, epi)
+    if (M <= 16) {
+      if (ksw == 1) CADENCE_STREAM(16, 1);
+      else if (ksw == 2) CADENCE_STREAM(16, 2);
+      else if (ksw == 4) CADENCE_STREAM(16, 4);
+      else CADENCE_STREAM(16, 10);
+    } else {
+      if (ksw == 1) CADENCE_STREAM(32, 1);
+      else if (ksw == 2) CADENCE_STREAM(32, 2);
+      else if (ksw == 4) CADENCE_STREAM(32, 4);
+      else CADENCE_STREAM(32, 10);
+    }
+#undef CADENCE_STREAM
+    if (ssplits > 1) {
+      int64_t outs = M * N;
+      int rblocks = (int)((outs + 255) / 256);
+      if (rblocks > 4096) rblocks = 4096;
+      hipLaunchKernelGGL((splitk_reduce_kernel<Epi>), dim3(rblocks, (unsigned)groups),
+                         dim3(256), 0, st, parts, ssplits, (int)groups, (int)M,
+                         (int)N, epi);
+    }
+    return (int)hipGetLastError();
+  }
+  if (!use_splitk_skinny()) {
+    const unsigned nblk = (unsigned)(Epi::kPaired ? N / 32 : N / 16);
+    dim3 grid(nblk, (unsigned)groups);
+    if (M <= 16)
+      hipLaunchKernelGGL((gemm_decode_kernel<16, Epi>), grid, dim3(512), 0, st, A,
+                         lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
+    else if (M <= 32)
+      hipLaunchKernelGGL((gemm_decode_kernel<32, Epi>), grid, dim3(512), 0, st, A,
+                         lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
+    else
+      hipLaunchKernelGGL((gemm_decode_kernel<64, Epi>), grid, dim3(512), 0, st, A,
+                         lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
+    return (int)hipGetLastError();
+  }
   const int splits = skinny_splits(N, K, groups);
   const int64_t klen = skinny_klen(K, splits);
   const int64_t need = (int64_t)splits * groups * M * N * 4;
@@ -644,7 +982,10 @@ int cadence_abi_version(void) { return 1; }
 
 int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
                                      int64_t groups) {
-  if (M > kSkinnyMaxM || M <= 0) return 0;
+  int ksw = 0, ss = 0;
+  if (M > 0 && stream_plan(M, K, &ksw, &ss))
+    return ss > 1 ? (int64_t)ss * groups * M * N * 4 : 0;
+  if (M > kSkinnyMaxM || M <= 0 || !use_splitk_skinny()) return 0;
   const int splits = skinny_splits(N, K, groups);
   return (int64_t)splits * groups * M * N * 4;
 }
@@ -723,7 +1064,7 @@ int cadence_gemm_patch_embed(const void* patches, int64_t ldp, const void* W,
 
 int64_t cadence_logits_scratch_bytes(int64_t M, int64_t V, int64_t D) {
   const int splits = skinny_splits(V, D, 1);
-  const int64_t nblk = (V + 255) / 256;
+  const int64_t nblk = (V + 15) / 16;   // >= the split-K path's V / 256 blocks
   return (int64_t)splits * M * V * 4 + M * nblk * 8 + 256;
 }
 
@@ -736,6 +1077,30 @@ int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
   if (scratch_bytes < cadence_logits_scratch_bytes(M, V, D))
     return (int)hipErrorInvalidValue;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!use_splitk_skinny()) {
+    const int64_t nblk = V / 16;
+    float* bval = static_cast<float*>(scratch);
+    int* bidx = reinterpret_cast<int*>(bval + M * nblk);
+    const u16* A = static_cast<const u16*>(X);
+    const u16* W = static_cast<const u16*>(E);
+    u16* lo = static_cast<u16*>(logits_out);
+    if (M <= 16)
+      hipLaunchKernelGGL(logits_decode_kernel<16>, dim3((unsigned)nblk), dim3(512), 0,
+                         st, A, ldx, W, D, (int)M, (int)V, (int)D, soft_cap, lo,
+                         bval, bidx);
+    else if (M <= 32)
+      hipLaunchKernelGGL(logits_decode_kernel<32>, dim3((unsigned)nblk), dim3(512), 0,
+                         st, A, ldx, W, D, (int)M, (int)V, (int)D, soft_cap, lo,
+                         bval, bidx);
+    else
+      hipLaunchKernelGGL(logits_decode_kernel<64>, dim3((unsigned)nblk), dim3(512), 0,
+                         st, A, ldx, W, D, (int)M, (int)V, (int)D, soft_cap, lo,
+                         bval, bidx);
+    if (next_token)
+      hipLaunchKernelGGL(argmax_final_kernel, dim3((unsigned)M), dim3(256), 0, st,
+                         bval, bidx, (int)nblk, next_token);
+    return (int)hipGetLastError();
+  }
   const int splits = skinny_splits(V, D, 1);
   const int64_t klen = skinny_klen(D, splits);
   float* part = static_cast<float*>(scratch);

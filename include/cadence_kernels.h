@@ -177,7 +177,15 @@ int cadence_segment_info(const int32_t* segment_pos, int32_t* seg_id,
  * q_out [M, H*hd], k_out/v_out [M, hd]. */
 int cadence_rope_qkv(const void* qkv, int64_t ldqkv, const int32_t* positions,
                      void* q_out, void* k_out, void* v_out, int64_t M,
-                     int64_t H, int64_t hd, void* stream);
+                     int64_t H, int64_t hd, const void* table,
+                     int64_t table_len, void* stream);
+
+/* sin / cos table for cadence_rope_qkv: table[p][0][i] = bf16(sin(p * f_i)),
+ * table[p][1][i] = bf16(cos(p * f_i)), i < hd / 4, f_i as modules.py:73-77
+ * computes it (fp32 inverse frequencies, fp32 angle).  Positions >= the
+ * table length are computed in-kernel instead. */
+int cadence_rope_table(void* table, int64_t positions, int64_t hd,
+                       void* stream);
 
 /* Prefill local MQA attention, flash-style (modules.py:466-480):
  * logits = bf16(q.k) * hd^-0.5, mask = same segment & causal & window,
