@@ -3,16 +3,22 @@
 //
 //   C[M, N] = A[M, K] . W[N, K]^T       (both operands K-contiguous)
 //
-// Two engines:
-//  * tile engine (prefill, M > 64): 128x128x64 block tile, 4 waves (2x2),
-//    wave tile 64x64 = 4x4 mfma_f32_16x16x32_bf16, register-staged
-//    double-buffered LDS with an XOR chunk swizzle (conflict-free
-//    ds_read_b128 / ds_write_b128), XCD-aware bijective block remap and a
-//    grouped tile order for L2 reuse.
-//  * skinny engine (decode, M <= 64): weight rows streamed once straight into
-//    MFMA B fragments, split-K over the grid, fp32 partial slabs reduced in a
-//    fixed order (deterministic) by a second kernel that applies the same
-//    epilogue.
+// Engines:
+//  * big tile engine (prefill, M > 64): 256x256x64 block tile, 8 waves (2x4),
+//    wave tile 128x64 of mfma_f32_16x16x32_bf16; operands go HBM -> LDS with
+//    global_load_lds (LDS-DMA, no VGPR staging), the XOR chunk swizzle is
+//    applied on the per-lane source address so ds_read_b128 stays
+//    conflict-free; double-buffered, one barrier per k-tile; XCD-aware
+//    bijective block remap + grouped tile order for L2 reuse.  Elementwise
+//    epilogues are staged through the freed LDS and written as 16-B rows.
+//  * stream engine (decode, M <= 32): every weight load of a block is issued
+//    up front (latency-bound regime), optionally split over K with the
+//    deterministic fp32 reduction below.
+//  * skinny engine (decode fallback / logits): weight rows streamed straight
+//    into MFMA B fragments, split-K over the grid, fp32 partial slabs reduced
+//    in a fixed order (deterministic) by a second kernel that applies the
+//    same epilogue.
+//  * legacy 128x128 register-staged tile engine (CADENCE_GEMM_LEGACY=1).
 //
 // Epilogues replicate the reference rounding points:
 //  EpiLinear      nn.Linear (+bias) [+GELU(erf)] [+residual], row remap
@@ -43,41 +49,70 @@ CADENCE_DEV float softcap(float l, float c) {
   return rbf(rbf(tanhf(t)) * c);
 }
 
+// Epilogue interface: apply / apply2 write one element (direct path);
+// staged epilogues (kStaged) split that into value / value2 (per element,
+// bf16-exact result before any residual) and store8 (8 consecutive output
+// columns of one row, 16-B aligned).
 struct EpiLinear {
   static constexpr bool kPaired = false;
+  static constexpr bool kStaged = true;
   u16* out; int64_t ldo;
   const u16* bias;
   const u16* resid; int64_t ldr;
   int act;                 // 0 none, 1 gelu(erf), 2 soft-cap(cap), 3 gelu(tanh)
   RowMap map;
   float cap;
-  CADENCE_DEV void apply(int64_t m, int n, float v, int) const {
+  CADENCE_DEV float value(int64_t, int n, float v, int) const {
     // F.linear adds the bias in fp32 before the single bf16 rounding.
     if (bias) v = add_rn(v, bf2f(bias[n]));
     float r = rbf(v);
     if (act == 1) r = rbf(gelu_erf(r));
     if (act == 2) r = softcap(r, cap);
     if (act == 3) r = rbf(gelu_tanh(r));
+    return r;
+  }
+  CADENCE_DEV void apply(int64_t m, int n, float v, int g) const {
+    float r = value(m, n, v, g);
     const int64_t orow = map(m);
     if (resid) r = badd(r, bf2f(resid[orow * ldr + n]));
     out[orow * ldo + n] = f2bf(r);
+  }
+  CADENCE_DEV void store8(int64_t m, int n, uint4 v, int) const {
+    const int64_t orow = map(m);
+    if (resid) {
+      float a[8], b[8];
+      unpack8(v, a);
+      unpack8(ld16(resid + orow * ldr + n), b);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = badd(a[i], b[i]);
+      v = pack8(a);
+    }
+    st16(out + orow * ldo + n, v);
   }
 };
 
 struct EpiGatedGelu {
   static constexpr bool kPaired = true;
+  static constexpr bool kStaged = true;
   u16* out; int64_t ldo;
   const u16* bias_g; const u16* bias_u;
-  CADENCE_DEV void apply2(int64_t m, int f, float g, float u, int) const {
+  CADENCE_DEV float value2(int64_t, int f, float g, float u, int) const {
     // Einsum result is rounded, then `+ b` rounds again (layers.py:729).
     g = badd(rbf(g), bf2f(bias_g[f]));
     u = badd(rbf(u), bf2f(bias_u[f]));
-    out[m * ldo + f] = f2bf(bmul(rbf(gelu_tanh(g)), u));
+    return bmul(rbf(gelu_tanh(g)), u);
+  }
+  CADENCE_DEV void apply2(int64_t m, int f, float g, float u, int gg) const {
+    out[m * ldo + f] = f2bf(value2(m, f, g, u, gg));
+  }
+  CADENCE_DEV void store8(int64_t m, int f, uint4 v, int) const {
+    st16(out + m * ldo + f, v);
   }
 };
 
 struct EpiRglruGates {
   static constexpr bool kPaired = true;
+  static constexpr bool kStaged = false;
   const u16* x; int64_t ldx;         // conv1d output (RG-LRU input)
   const u16* bias_x; const u16* bias_a;
   const u16* softplus_a;             // bf16(softplus(a_param)), [E]
@@ -101,6 +136,7 @@ struct EpiRglruGates {
 
 struct EpiVitResid {
   static constexpr bool kPaired = false;
+  static constexpr bool kStaged = false;
   float* resid; int64_t ldr;
   const u16* bias; const u16* gamma;
   CADENCE_DEV void apply(int64_t m, int n, float v, int) const {
@@ -112,6 +148,7 @@ struct EpiVitResid {
 
 struct EpiPatch {
   static constexpr bool kPaired = false;
+  static constexpr bool kStaged = false;
   float* resid;                      // [B, ntok, N] fp32
   const u16* bias; const u16* pos;   // pos [P, N]
   int64_t P, ntok, prefix, N;
@@ -365,7 +402,49 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
 
   const int mbase = m0 + wm * 128, nbase = n0 + wn * 64;
   const int rsub = (lane >> 4) * 4, csub = lane & 15;
-  if constexpr (Epi::kPaired) {
+  if constexpr (Epi::kStaged) {
+    // Stage the wave's bf16 results in its own 16 KiB of the (now idle)
+    // operand LDS, [128 rows][OC cols] with a 16-B chunk XOR swizzle, then
+    // write whole 16-B row segments (one store instruction per 8 rows).
+    constexpr int OC = Epi::kPaired ? 32 : 64;     // output columns per wave
+    constexpr int CPRW = OC / 8;                   // 16-B chunks per row
+    __syncthreads();   // every wave is done reading the operand buffers
+    if (nbase >= N) return;   // wave-uniform: this wave's columns are padding
+    u16* st = reinterpret_cast<u16*>(smem) + wave * (128 * 64);
+    auto sidx = [&](int r, int c) {
+      return r * OC + (((c >> 3) ^ (r & (CPRW - 1))) << 3) + (c & 7);
+    };
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < (Epi::kPaired ? 2 : NR); ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = i * 16 + rsub + r;
+          const int lc = j * 16 + csub;
+          float v;
+          if constexpr (Epi::kPaired)
+            v = epi.value2(mbase + lr, nbase / 2 + lc, acc[i][j][r],
+                           acc[i][j + 2][r], g);
+          else
+            v = epi.value(mbase + lr, min(nbase + lc, N - 1), acc[i][j][r], g);
+          st[sidx(lr, lc)] = f2bf(v);
+        }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    constexpr int RPI = 64 / CPRW;                 // rows per store instruction
+    const int obase = Epi::kPaired ? nbase / 2 : nbase;
+#pragma unroll
+    for (int it = 0; it < 128 / RPI; ++it) {
+      const int lr = it * RPI + lane / CPRW;
+      const int ch = lane % CPRW;
+      const int row = mbase + lr;
+      const int col = obase + ch * 8;
+      const uint4 v = *reinterpret_cast<const uint4*>(
+          &st[lr * OC + ((ch ^ (lr & (CPRW - 1))) << 3)]);
+      if (row < M && (Epi::kPaired || col < N)) epi.store8(row, col, v, g);
+    }
+  } else if constexpr (Epi::kPaired) {
 #pragma unroll
     for (int i = 0; i < MR; ++i)
 #pragma unroll
