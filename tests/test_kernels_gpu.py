@@ -51,17 +51,27 @@ def test_rnn_scan_bitexact(dev, b, t, e, with_h0):
   assert torch.equal(h.cpu(), h_ref)
 
 
-def test_rnn_scan_gated_matches_join(dev):
-  """scan(x, a) * gate fused == reference rnn_scan then `x * y`."""
+@pytest.mark.parametrize("t,e,strided,with_h0", [(70, 512, False, False),
+                                                 (300, 2560, True, True),
+                                                 (2048, 256, True, False),
+                                                 (33, 192, True, True)])
+def test_rnn_scan_gated_matches_join(dev, t, e, strided, with_h0):
+  """scan(x, a) * gate fused == reference rnn_scan then `x * y`; the gate may
+  be the y half of the packed [y | x] GEMM output (row stride 2E)."""
   g = torch.Generator().manual_seed(1)
-  b, t, e = 2, 70, 512
-  x, gate = rnd(b, t, e, gen=g), rnd(b, t, e, gen=g)
+  b = 2
+  x = rnd(b, t, e, gen=g)
+  yx = rnd(b * t, 2 * e, gen=g)
+  gate = yx[:, :e] if strided else yx[:, :e].contiguous()
   a = torch.rand(b, t, e, generator=g).to(BF)
-  pos = two_doc_positions(b, t, 30)
-  y_ref, h_ref = R.rnn_scan(x, a, pos == 0, None)
-  want = y_ref * gate
+  pos = two_doc_positions(b, t, t // 2 + 1)
+  h0 = torch.randn(b, e, generator=g) if with_h0 else None
+  y_ref, h_ref = R.rnn_scan(x, a, pos == 0, h0)
+  want = y_ref * gate.reshape(b, t, e)
+  gate_d = yx.to(dev)[:, :e] if strided else gate.to(dev)
   got, h = ops.ops.rnn_scan(x.view(-1, e).to(dev), a.view(-1, e).to(dev),
-                            pos.to(dev), None, gate.view(-1, e).to(dev), b, t)
+                            pos.to(dev), None if h0 is None else h0.to(dev),
+                            gate_d, b, t)
   assert torch.equal(got.view(b, t, e).cpu(), want)
   assert torch.equal(h.cpu(), h_ref)
 

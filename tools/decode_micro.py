@@ -26,10 +26,10 @@ def main():
   _, cache = model(tok[:, :-1], pos[:, :-1], return_logits=False)
   nxt, _, cache = model.next_token(tok[:, -1:], pos[:, -1:], cache)
   engines = {}
-  for mode in ("stream", "splitk"):
+  for mode in os.environ.get("ENGINES", "stream,splitk").split(","):
     os.environ["CADENCE_DECODE_ENGINE"] = mode
     engines[mode] = S._DecodeGraph(model, cache, b, 64, dev)
-  reps = 20
+  reps = int(os.environ.get("REPS", "20"))
   for rnd in range(2):
     for mode, eng in engines.items():
       for dst, src in ((eng.cur, nxt), (eng.pos, pos[:, -1] + 1)):
