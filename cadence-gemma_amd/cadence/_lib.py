@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 3
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -32,17 +32,17 @@ _SIGS: dict[str, list] = {
     "cadence_gemm_workspace_bytes": [I64, I64, I64, I64],
     "cadence_gemm_linear": [P, I64, P, I64, P, P, I64, P, I64, I64, I64, I64,
                             I32, I64, I64, I64, P, I64, P],
-    "cadence_gemm_gated_gelu": [P, I64, P, P, P, P, I64, I64, I64, I64, P, I64,
-                                P],
-    "cadence_rglru_gates": [P, I64, P, P, P, P, P, P, P, I64, I64, I64, I64, P,
-                            I64, P],
+    "cadence_gemm_gated_gelu": [P, I64, P, I64, P, P, P, I64, I64, I64, I64, P,
+                                I64, P],
+    "cadence_rglru_gates": [P, I64, P, I64, P, P, P, P, P, P, I64, I64, I64, I64,
+                            P, I64, P],
     "cadence_gemm_vit_residual": [P, I64, P, I64, P, P, P, I64, I64, I64, I64,
                                   P, I64, P],
     "cadence_gemm_patch_embed": [P, I64, P, I64, P, P, P, I64, I64, I64, I64,
                                  I64, I64, P, I64, P],
-    "cadence_logits_argmax": [P, I64, P, I64, I64, I64, F32, P, P, P, I64, P],
+    "cadence_logits_argmax": [P, I64, P, I64, I64, I64, I64, F32, P, P, P, I64, P],
     "cadence_logits_scratch_bytes": [I64, I64, I64],
-    "cadence_gemm_logits": [P, I64, P, I64, I64, I64, F32, P, I64, P, I64, P],
+    "cadence_gemm_logits": [P, I64, P, I64, I64, I64, I64, F32, P, I64, P, I64, P],
     "cadence_rmsnorm": [P, I64, P, P, I64, I64, I64, F32, P],
     "cadence_layernorm": [P, I64, P, P, P, I64, I64, I64, F32, P],
     "cadence_embed": [P, P, P, I64, I64, I64, F32, I64, I64, I64, P],
@@ -56,7 +56,8 @@ _SIGS: dict[str, list] = {
     "cadence_local_attention": [P, P, P, P, P, P, I64, I64, I64, I64, I64, P],
     "cadence_kv_cache_fill": [P, P, P, P, P, P, I64, I64, I64, I64, P],
     "cadence_local_attention_decode": [P, P, P, P, P, P, P, I64, I64, I64, I64,
-                                       P],
+                                       P, I64, P, P],
+    "cadence_local_attention_decode_workspace_bytes": [I64, I64],
     "cadence_im2col_normalize": [P, P, I64, I64, I64, I64, P, P, P],
     "cadence_vit_prefix": [P, P, I64, I64, I64, I64, P],
     "cadence_vit_attention": [P, P, I64, I64, I64, I64, P],
@@ -66,6 +67,7 @@ _SIGS: dict[str, list] = {
 }
 _RESTYPE = {
     "cadence_gemm_workspace_bytes": I64,
+    "cadence_local_attention_decode_workspace_bytes": I64,
     "cadence_logits_scratch_bytes": I64,
 }
 

@@ -136,8 +136,8 @@ class Griffin(nn.Module):
     if not return_logits:
       return None, new_cache
     xn = ops.rmsnorm(x, self.final_norm.scale, self.final_norm.eps)
-    logits = ops.ops.gemm_logits(xn, self.embedder.input_embedding,
-                                 float(self.config.logits_soft_cap or 0.0))
+    logits = ops.gemm_logits(xn, self.embedder.input_embedding,
+                             float(self.config.logits_soft_cap or 0.0))
     return logits.view(b, length, -1), new_cache
 
   @torch.no_grad()
@@ -155,7 +155,7 @@ class Griffin(nn.Module):
                                   segment_pos.reshape(b, 1))
     x, new_cache = self.run_blocks(x, pos, b, 1, cache, True, inplace)
     xn = ops.rmsnorm(x, self.final_norm.scale, self.final_norm.eps)
-    logits, nxt = ops.ops.logits_argmax(
+    logits, nxt = ops.logits_argmax(
         xn, self.embedder.input_embedding,
         float(self.config.logits_soft_cap or 0.0), return_logits)
     return nxt, (logits if return_logits else None), new_cache

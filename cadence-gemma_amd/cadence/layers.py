@@ -184,7 +184,7 @@ class RGLRU(nn.Module):
   def gates(self, x2d: torch.Tensor, pos_flat: torch.Tensor):
     """Fused BDL x2 + gate chain -> (a with resets zeroed, normalized x)."""
     w, bx, ba, sp = self.packed()
-    return ops.ops.rglru_gates(x2d, w, bx, ba, sp, pos_flat)
+    return ops.rglru_gates(x2d, w, bx, ba, sp, pos_flat)
 
   def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,
               cache: torch.Tensor | None = None, return_cache: bool = True):

@@ -258,7 +258,7 @@ class MLPBlock(nn.Module):
 
   def fused(self, xn2d, resid2d):
     w, bg, bu = self.ffw_up.gated_packed()
-    act = ops.ops.gated_gelu(xn2d, w, bg, bu)
+    act = ops.gated_gelu(xn2d, w, bg, bu)
     return ops.linear(act, self.ffw_down.weight, self.ffw_down.bias,
                       resid=resid2d)
 
@@ -386,5 +386,5 @@ class Embedder(nn.Module):
     return out.view(*x.shape, self.embed_dim)
 
   def decode(self, x: torch.Tensor) -> torch.Tensor:
-    logits = ops.ops.gemm_logits(_flat(x), self.input_embedding, 0.0)
+    logits = ops.gemm_logits(_flat(x), self.input_embedding, 0.0)
     return logits.view(*x.shape[:-1], self.vocab_size)

@@ -105,6 +105,22 @@ def _tile(M: int) -> bool:
   return M > 64
 
 
+_COUNTERS: dict[int, torch.Tensor] = {}
+
+
+def _counters(dev: torch.device, n: int):
+  """Zeroed int32 arrival counters of `dev` for the in-kernel split combines
+  (kernels leave them at zero); None while capturing before first use."""
+  idx = dev.index if dev.index is not None else torch.cuda.current_device()
+  buf = _COUNTERS.get(idx)
+  if buf is None or buf.numel() < n:
+    if torch.cuda.is_current_stream_capturing():
+      return None
+    buf = torch.zeros(max(n, 4096), dtype=torch.int32, device=dev)
+    _COUNTERS[idx] = buf
+  return buf
+
+
 def _ws(M: int, N: int, K: int, groups: int, like: torch.Tensor):
   n = _lib.load().cadence_gemm_workspace_bytes(M, N, K, groups)
   if n == 0:
@@ -114,10 +130,49 @@ def _ws(M: int, N: int, K: int, groups: int, like: torch.Tensor):
 
 # ------------------------------------------------------------------- GEMMs
 
+# ------------------------------------------------- decode weight layout
+
+def pack_decode(w: torch.Tensor) -> torch.Tensor:
+  """Fragment-packed copy of a [.., N, K] weight (cadence_kernels.h "Decode
+  weight layout"): per 16-row x 32-column tile, the 64 MFMA lanes' 16-B
+  fragments back to back, so decode GEMMs stream 1 KiB per wave load."""
+  *g, n, k = w.shape
+  _need(n % 16 == 0 and k % 32 == 0, "decode packing needs N % 16, K % 32")
+  return (w.reshape(*g, n // 16, 16, k // 32, 4, 8).movedim(-4, -2)
+          .contiguous().view(w.shape))
+
+
+def decode_weight(w: torch.Tensor):
+  """The cached fragment-packed copy of `w` for M <= 32 launches (rebuilt
+  when `w` changes), or None when it cannot be packed or would be built
+  inside a graph capture."""
+  if w.dim() < 2 or w.shape[-2] % 16 or w.shape[-1] % 32 or not w.is_cuda:
+    return None
+  c = getattr(w, "_cadence_decode", None)
+  key = (w.data_ptr(), w._version)
+  if c is not None and c[0] == key:
+    return c[1]
+  if torch.cuda.is_current_stream_capturing():
+    return None
+  with torch.no_grad():
+    packed = pack_decode(w.detach())
+  w._cadence_decode = (key, packed)
+  return packed
+
+
+def _wld(w, packed: bool, name: str) -> int:
+  if packed:
+    _need(w.is_contiguous() and w.dtype == _BF16, f"{name}: packed layout")
+    return 0
+  return _mat(w, name)
+
+
 @_reg("gemm_linear_(Tensor a, Tensor w, Tensor? bias, Tensor? resid, "
-      "Tensor(a!) out, int act, int row_div, int row_mul, int row_off) -> ()")
-def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off):
-  lda, ldw, ldo = _mat(a, "a"), _mat(w, "w"), _mat(out, "out")
+      "Tensor(a!) out, int act, int row_div, int row_mul, int row_off, "
+      "bool w_packed=False) -> ()")
+def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off,
+                 w_packed=False):
+  lda, ldw, ldo = _mat(a, "a"), _wld(w, w_packed, "w"), _mat(out, "out")
   M, K = a.shape
   N = w.shape[0]
   _need(w.shape[1] == K, f"K mismatch {K} vs {w.shape[1]}")
@@ -135,8 +190,8 @@ def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off):
 
 
 @_reg("gated_gelu(Tensor a, Tensor w_packed, Tensor bias_gate, "
-      "Tensor bias_up) -> Tensor")
-def _gated_gelu(a, w_packed, bias_gate, bias_up):
+      "Tensor bias_up, bool decode_layout=False) -> Tensor")
+def _gated_gelu(a, w_packed, bias_gate, bias_up, decode_layout=False):
   lda = _mat(a, "a")
   M, K = a.shape
   F = w_packed.shape[0] // 2
@@ -145,15 +200,17 @@ def _gated_gelu(a, w_packed, bias_gate, bias_up):
   ws, nws = _ws(M, 2 * F, K, 1, a)
   ev = TIMER.start(a) if _tile(M) else None
   _lib.check(_lib.load().cadence_gemm_gated_gelu(
-      _p(a), lda, _p(w_packed), _p(bias_gate), _p(bias_up), _p(out), F, M, F,
-      K, _p(ws), nws, _s(a)), "gated_gelu")
+      _p(a), lda, _p(w_packed), 0 if decode_layout else K, _p(bias_gate),
+      _p(bias_up), _p(out), F, M, F, K, _p(ws), nws, _s(a)), "gated_gelu")
   TIMER.stop(ev, "gemm_tile_kernel<EpiGatedGelu>", 4.0 * M * F * K, a)
   return out
 
 
 @_reg("rglru_gates(Tensor x, Tensor w_packed, Tensor bias_x, Tensor bias_a, "
-      "Tensor softplus_a, Tensor segment_pos) -> (Tensor, Tensor)")
-def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos):
+      "Tensor softplus_a, Tensor segment_pos, bool decode_layout=False) "
+      "-> (Tensor, Tensor)")
+def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos,
+                 decode_layout=False):
   ldx = _mat(x, "x")
   M, E = x.shape
   H, two_bw, bw = w_packed.shape
@@ -164,8 +221,9 @@ def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos):
   ws, nws = _ws(M, 2 * bw, bw, H, x)
   ev = TIMER.start(x) if _tile(M) else None
   _lib.check(_lib.load().cadence_rglru_gates(
-      _p(x), ldx, _p(w_packed), _p(bias_x), _p(bias_a), _p(softplus_a),
-      _p(segment_pos.contiguous()), _p(a), _p(nx), E, M, H, bw, _p(ws), nws,
+      _p(x), ldx, _p(w_packed), 0 if decode_layout else bw, _p(bias_x),
+      _p(bias_a), _p(softplus_a), _p(segment_pos.contiguous()), _p(a), _p(nx),
+      E, M, H, bw, _p(ws), nws,
       _s(x)), "rglru_gates")
   TIMER.stop(ev, "gemm_tile_kernel<EpiRglruGates>", 2.0 * M * 2 * bw * bw * H, x)
   return a, nx
@@ -199,8 +257,8 @@ def _patch_embed(patches, w, bias, pos, resid, B, P, ntok, prefix):
 
 
 @_reg("logits_argmax(Tensor x, Tensor embedding, float soft_cap, "
-      "bool return_logits) -> (Tensor, Tensor)")
-def _logits_argmax(x, embedding, soft_cap, return_logits):
+      "bool return_logits, bool decode_layout=False) -> (Tensor, Tensor)")
+def _logits_argmax(x, embedding, soft_cap, return_logits, decode_layout=False):
   ldx = _mat(x, "x")
   M, D = x.shape
   V = embedding.shape[0]
@@ -211,22 +269,24 @@ def _logits_argmax(x, embedding, soft_cap, return_logits):
                        device=x.device)
   nxt = torch.empty(M, dtype=_I32, device=x.device)
   _lib.check(L.cadence_logits_argmax(
-      _p(x), ldx, _p(embedding), M, V, D, float(soft_cap),
-      _p(logits) if return_logits else None, _p(nxt), _p(scratch), nscr,
+      _p(x), ldx, _p(embedding), 0 if decode_layout else D, M, V, D,
+      float(soft_cap), _p(logits) if return_logits else None, _p(nxt),
+      _p(scratch), nscr,
       _s(x)), "logits_argmax")
   return logits, nxt
 
 
-@_reg("gemm_logits(Tensor x, Tensor embedding, float soft_cap) -> Tensor")
-def _gemm_logits(x, embedding, soft_cap):
+@_reg("gemm_logits(Tensor x, Tensor embedding, float soft_cap, "
+      "bool decode_layout=False) -> Tensor")
+def _gemm_logits(x, embedding, soft_cap, decode_layout=False):
   ldx = _mat(x, "x")
   M, D = x.shape
   V = embedding.shape[0]
   out = torch.empty(M, V, dtype=_BF16, device=x.device)
   ws, nws = _ws(M, V, D, 1, x)
   _lib.check(_lib.load().cadence_gemm_logits(
-      _p(x), ldx, _p(embedding), M, V, D, float(soft_cap), _p(out), V, _p(ws),
-      nws, _s(x)), "gemm_logits")
+      _p(x), ldx, _p(embedding), 0 if decode_layout else D, M, V, D,
+      float(soft_cap), _p(out), V, _p(ws), nws, _s(x)), "gemm_logits")
   return out
 
 
@@ -420,9 +480,14 @@ def _local_attention_decode(q, k_new, v_new, cache_k, cache_v, num_tokens, H):
   _need(cache_k.is_contiguous() and cache_v.is_contiguous(), "cache layout")
   _need(num_tokens.dtype == _I32, "num_tokens int32")
   out = torch.empty(B, H * hd, dtype=_BF16, device=q.device)
-  _lib.check(_lib.load().cadence_local_attention_decode(
+  lib = _lib.load()
+  nws = lib.cadence_local_attention_decode_workspace_bytes(B, hd)
+  ws = torch.empty(nws, dtype=torch.uint8, device=q.device)
+  sems = _counters(q.device, B)
+  _lib.check(lib.cadence_local_attention_decode(
       _p(q.contiguous()), _p(k_new.contiguous()), _p(v_new.contiguous()),
-      _p(cache_k), _p(cache_v), _p(num_tokens), _p(out), B, H, hd, W, _s(q)),
+      _p(cache_k), _p(cache_v), _p(num_tokens), _p(out), B, H, hd, W,
+      _p(ws) if sems is not None else None, nws, _p(sems), _s(q)),
       "local_attention_decode")
   return out
 
@@ -509,8 +574,41 @@ def linear(x2d, w, bias=None, act=0, resid=None, out=None,
   if out is None:
     out = torch.empty(M, N, dtype=_BF16, device=x2d.device)
   div, mul, off = row_map if row_map is not None else (max(M, 1), 0, 0)
-  ops.gemm_linear_(x2d, w, bias, resid, out, act, div, mul, off)
+  wd = decode_weight(w) if M <= 32 else None
+  if wd is not None:
+    ops.gemm_linear_(x2d, wd, bias, resid, out, act, div, mul, off, True)
+  else:
+    ops.gemm_linear_(x2d, w, bias, resid, out, act, div, mul, off)
   return out
+
+
+def gated_gelu(x2d, w_packed, bias_gate, bias_up):
+  """MLP up + gate (packed [2F, K] weight); decode rows use its packed copy."""
+  wd = decode_weight(w_packed) if x2d.shape[0] <= 32 else None
+  if wd is not None:
+    return ops.gated_gelu(x2d, wd, bias_gate, bias_up, True)
+  return ops.gated_gelu(x2d, w_packed, bias_gate, bias_up)
+
+
+def rglru_gates(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat):
+  wd = decode_weight(w_packed) if x2d.shape[0] <= 32 else None
+  if wd is not None:
+    return ops.rglru_gates(x2d, wd, bias_x, bias_a, softplus_a, pos_flat, True)
+  return ops.rglru_gates(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat)
+
+
+def logits_argmax(x2d, embedding, soft_cap, return_logits):
+  wd = decode_weight(embedding) if x2d.shape[0] <= 32 else None
+  if wd is not None:
+    return ops.logits_argmax(x2d, wd, soft_cap, return_logits, True)
+  return ops.logits_argmax(x2d, embedding, soft_cap, return_logits)
+
+
+def gemm_logits(x2d, embedding, soft_cap):
+  wd = decode_weight(embedding) if x2d.shape[0] <= 32 else None
+  if wd is not None:
+    return ops.gemm_logits(x2d, wd, soft_cap, True)
+  return ops.gemm_logits(x2d, embedding, soft_cap)
 
 
 def rmsnorm(x2d, scale, eps=1e-6):

@@ -22,6 +22,7 @@ namespace {
 constexpr int MODE_LOCAL = 0;
 constexpr int MODE_VIT = 1;
 constexpr int KT = 32;  // keys per tile
+constexpr int kDecodeSplits = 8;  // window splits of the decode attention
 
 struct AttnArgs {
   const u16* q; int64_t q_bs, q_rs, q_hs;   // batch / row / head strides
@@ -237,18 +238,33 @@ struct DecodeArgs {
   u16* o;                 // [B, H*hd]
   int H, hd, W;
   float scale;
+  float* parts;           // [B, NS, 32 + 16 * hd] fp32 split partials (NS > 1)
+  int32_t* sems;          // [B] zeroed arrival counters (NS > 1)
 };
 
-// 4 waves per sequence: all stage the K / V^T tiles, each computes the
+// 4 waves per (sequence, window split): all stage the K / V^T tiles, each computes the
 // (cheap) 16 x 32 score tile and softmax redundantly, and each owns a
 // quarter of the head dim in P.V and in the output.
+//
+// Split over the window (gridDim.y = NS): split s takes its share of the
+// non-empty key tiles (the ring tiles below the fill level plus the tile of
+// the new key), keeps its own online-softmax state, and publishes
+// (m, l, unnormalised o) per query row with write-through stores; the last
+// split to arrive at the sequence's counter combines the NS partials in
+// split order (fixed, so replays are bit-identical), writes the output and
+// performs the cache update.  Hand-off: MI355X_MICROARCH "inter-workgroup
+// visibility", first protocol row (sc1 stores and loads, one relaxed agent
+// atomic per workgroup, no fences).
 template <int HD>
 __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
   constexpr int KS = HD / 32, NO = HD / 16 / 4, CPR = HD / 8;
   __shared__ uint4 ks_[KT * HD / 8];
   __shared__ u16 vt[HD * KT];
   __shared__ u16 ptall[4][16 * KT];
+  __shared__ int ticket;
+  __shared__ __attribute__((aligned(16))) float ml[32];   // split m[16], l[16]
   const int b = blockIdx.x;
+  const int split = blockIdx.y, NS = gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   u16* pt = ptall[wave];
   const int dbase = wave * NO * 16;
@@ -282,9 +298,15 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
   const u16* ckb = a.ck + (int64_t)b * a.W * a.hd;
   const u16* cvb = a.cv + (int64_t)b * a.W * a.hd;
 
-  // iterate tiles over [0, slot_hi) and the final tile holding the new key
-  for (int k0 = 0; k0 < nslots; k0 += KT) {
-    if (k0 >= slot_hi && k0 + KT <= a.W) continue;  // no valid slot in tile
+  // non-empty tiles: ring tiles below slot_hi, then the tile of slot W
+  const int ring_tiles = (slot_hi + KT - 1) / KT;
+  const int last_tile = a.W / KT;
+  const int ntot = last_tile < ring_tiles ? ring_tiles : ring_tiles + 1;
+  const int tps = (ntot + NS - 1) / NS;
+  const int tb = min(ntot, split * tps), te = min(ntot, tb + tps);
+  (void)nslots;
+  for (int ti = tb; ti < te; ++ti) {
+    const int k0 = (ti < ring_tiles ? ti : last_tile) * KT;
     __syncthreads();
     for (int c = tid; c < KT * CPR; c += 256) {
       const int kr = c / CPR, ch = c % CPR;
@@ -379,19 +401,88 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
       o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[j], 0, 0, 0);
     }
   }
+  if (NS == 1) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int hrow = 4 * (lane >> 4) + r;
-    if (hrow >= a.H) continue;
-    const float inv = l_run[r] > 0.0f ? 1.0f / l_run[r] : 0.0f;
+    for (int r = 0; r < 4; ++r) {
+      const int hrow = 4 * (lane >> 4) + r;
+      if (hrow >= a.H) continue;
+      const float inv = l_run[r] > 0.0f ? 1.0f / l_run[r] : 0.0f;
 #pragma unroll
-    for (int j = 0; j < NO; ++j) {
-      const int d = dbase + j * 16 + (lane & 15);
-      a.o[(int64_t)b * a.H * a.hd + hrow * a.hd + d] = f2bf(o[j][r] * inv);
+      for (int j = 0; j < NO; ++j) {
+        const int d = dbase + j * 16 + (lane & 15);
+        a.o[(int64_t)b * a.H * a.hd + hrow * a.hd + d] = f2bf(o[j][r] * inv);
+      }
     }
+  } else {
+    constexpr int PS = 32 + 16 * HD;            // floats per split partial
+    float* part = a.parts + ((int64_t)b * NS + split) * PS;
+    float* stage = reinterpret_cast<float*>(ks_);   // [16][HD] fp32 = sizeof(ks_)
+    __syncthreads();
+    if (tb < te) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hrow = 4 * (lane >> 4) + r;
+#pragma unroll
+        for (int j = 0; j < NO; ++j)
+          stage[hrow * HD + dbase + j * 16 + (lane & 15)] = o[j][r];
+        if (wave == 0 && (lane & 15) == 0) {
+          ml[hrow] = m_run[r];
+          ml[16 + hrow] = l_run[r];
+        }
+      }
+    }
+    __syncthreads();
+    if (tb < te) {
+      for (int q = tid * 4; q < PS; q += 1024) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(q < 32 ? ml + q : stage + (q - 32));
+        float* dst = part + q;
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(dst), "v"(v) : "memory");
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      ticket = __hip_atomic_fetch_add(&a.sems[b], 1, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (ticket != NS - 1) return;
+    const int nsp = (ntot + tps - 1) / tps;     // splits that held tiles
+    const float* pb = a.parts + (int64_t)b * NS * PS;
+    for (int q = tid * 4; q < 16 * HD; q += 1024) {
+      const int hrow = q / HD;
+      if (hrow >= a.H) continue;
+      float mx = -INFINITY;
+      for (int sp = 0; sp < nsp; ++sp)
+        mx = fmaxf(mx, __hip_atomic_load(pb + sp * PS + hrow, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT));
+      float l = 0.0f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < nsp; ++sp) {
+        const float ms = __hip_atomic_load(pb + sp * PS + hrow, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        const float ls = __hip_atomic_load(pb + sp * PS + 16 + hrow, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        const float wgt = (ms == -INFINITY) ? 0.0f : expf(ms - mx);
+        l += ls * wgt;
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(pb + sp * PS + 32 + q);
+        const uint64_t w0 = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t w1 = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[0] += __uint_as_float((uint32_t)w0) * wgt;
+        acc[1] += __uint_as_float((uint32_t)(w0 >> 32)) * wgt;
+        acc[2] += __uint_as_float((uint32_t)w1) * wgt;
+        acc[3] += __uint_as_float((uint32_t)(w1 >> 32)) * wgt;
+      }
+      const float inv = l > 0.0f ? 1.0f / l : 0.0f;
+      u16* dst = a.o + (int64_t)b * a.H * a.hd + q;
+      const uint32_t lo = (uint32_t)f2bf(acc[0] * inv) | ((uint32_t)f2bf(acc[1] * inv) << 16);
+      const uint32_t hi = (uint32_t)f2bf(acc[2] * inv) | ((uint32_t)f2bf(acc[3] * inv) << 16);
+      *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+    }
+    if (tid == 0)
+      __hip_atomic_store(&a.sems[b], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // _update_attention_cache: write the new key/value into slot nt % W, then
-  // bump num_tokens (all reads of this sequence's cache are done).
+  // bump num_tokens (all reads of this sequence's cache are done: with NS > 1
+  // every split has arrived before the last one gets here).
   __syncthreads();
   const int slot = nt % a.W;
   for (int d = tid * 8; d < a.hd; d += 2048) {
@@ -607,26 +698,35 @@ int cadence_kv_cache_fill(const void* k, const void* v,
   return (int)hipGetLastError();
 }
 
+int64_t cadence_local_attention_decode_workspace_bytes(int64_t B, int64_t hd) {
+  return B * kDecodeSplits * (32 + 16 * hd) * 4;
+}
+
 int cadence_local_attention_decode(const void* q, const void* k_new,
                                    const void* v_new, void* cache_k,
                                    void* cache_v, int32_t* num_tokens,
                                    void* out, int64_t B, int64_t H,
-                                   int64_t hd, int64_t window, void* stream) {
+                                   int64_t hd, int64_t window, void* workspace,
+                                   int64_t ws_bytes, int32_t* sems, void* stream) {
   if ((hd != 256 && hd != 128 && hd != 64) || H > 16)
     return (int)hipErrorInvalidValue;
   if (B <= 0) return 0;
+  const bool split = workspace && sems &&
+                     ws_bytes >= cadence_local_attention_decode_workspace_bytes(B, hd);
   DecodeArgs a{static_cast<const u16*>(q), static_cast<const u16*>(k_new),
                static_cast<const u16*>(v_new), hd,
                static_cast<u16*>(cache_k), static_cast<u16*>(cache_v),
                num_tokens, static_cast<u16*>(out), (int)H, (int)hd,
-               (int)window, 1.0f / sqrtf((float)hd)};
+               (int)window, 1.0f / sqrtf((float)hd),
+               static_cast<float*>(workspace), sems};
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)B, split ? kDecodeSplits : 1);
   if (hd == 256)
-    hipLaunchKernelGGL(decode_attn_kernel<256>, dim3((unsigned)B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(decode_attn_kernel<256>, grid, dim3(256), 0, st, a);
   else if (hd == 128)
-    hipLaunchKernelGGL(decode_attn_kernel<128>, dim3((unsigned)B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(decode_attn_kernel<128>, grid, dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(decode_attn_kernel<64>, dim3((unsigned)B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(decode_attn_kernel<64>, grid, dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -58,6 +58,12 @@ struct alignas(16) u16x8 {
 };
 
 CADENCE_DEV uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+// Non-temporal 16-B load for bytes read once (decode weights): `nt` policy.
+CADENCE_DEV uint4 ld16_nt(const void* p) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 CADENCE_DEV void st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
 
 CADENCE_DEV void unpack8(uint4 v, float (&f)[8]) {

@@ -26,6 +26,9 @@
 //  EpiRglruGates  RG-LRU gate chain -> (a, normalized_x)       layers.py:345-365
 //  EpiVitResid    timm residual: resid += gamma * (x.W + b)   (fp32 stream)
 //  EpiPatch       patch-embed conv as GEMM + pos_embed at a prefix offset
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include "common.hpp"
 #include "../../include/cadence_kernels.h"
@@ -470,102 +473,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
   }
 }
 
-// ---------------------------------------------------------- decode engine
-//
-// M <= 64 rows (decode batch).  One workgroup = 16 output columns (paired
-// epilogues: the 16 gate + 16 up packed columns of 16 outputs), 8 waves
-// stride over K in 32-deep steps, each weight byte is read exactly once
-// straight into MFMA B fragments (no LDS staging), A (the activations,
-// L2-resident) likewise.  Partial accumulators are summed through LDS in a
-// fixed wave order (deterministic) and the epilogue is applied in the same
-// kernel: no split-K slabs, no reduce launch.
-
-template <int MS, class Epi>
-__global__ __launch_bounds__(512) void gemm_decode_kernel(
-    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
-    int64_t ldw, int M, int N, int K, int64_t a_goff, int64_t w_goff,
-    Epi epi) {
-  constexpr int MR = MS / 16;
-  constexpr int NREP = Epi::kPaired ? 2 : 1;
-  constexpr int U = 4;
-  __shared__ float red[8][MS * 16 * NREP];
-  const int g = blockIdx.y;
-  A += g * a_goff;
-  W += g * w_goff;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int col[NREP];
-  if constexpr (Epi::kPaired) {
-    const int grp = blockIdx.x >> 1, half = blockIdx.x & 1;
-    col[0] = grp * 64 + half * 16;
-    col[NREP - 1] = grp * 64 + 32 + half * 16;
-  } else {
-    col[0] = blockIdx.x * 16;
-  }
-  const int koff = 8 * (lane >> 4);
-  const int ksteps = K / 32;
-  f32x4 acc[MR][NREP];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const uint4 zero = make_uint4(0, 0, 0, 0);
-  const u16* wrow[NREP];
-#pragma unroll
-  for (int j = 0; j < NREP; ++j)
-    wrow[j] = W + (int64_t)(col[j] + (lane & 15)) * ldw + koff;
-  for (int ks0 = wave; ks0 < ksteps; ks0 += 8 * U) {
-    uint4 wb[U][NREP], xa[U][MR];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int ks = ks0 + 8 * u;
-      const bool ok = ks < ksteps;
-      const int k = ks * 32;
-#pragma unroll
-      for (int j = 0; j < NREP; ++j) wb[u][j] = ok ? ld16(wrow[j] + k) : zero;
-#pragma unroll
-      for (int i = 0; i < MR; ++i) {
-        const int m = i * 16 + (lane & 15);
-        xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + k + koff) : zero;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-#pragma unroll
-        for (int j = 0; j < NREP; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, xa[u][i]),
-              __builtin_bit_cast(bf16x8, wb[u][j]), acc[i][j], 0, 0, 0);
-  }
-  const int rsub = (lane >> 4) * 4, csub = lane & 15;
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NREP; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        red[wave][((i * 16 + rsub + r) * NREP + j) * 16 + csub] = acc[i][j][r];
-  __syncthreads();
-  for (int o = threadIdx.x; o < MS * 16; o += 512) {
-    const int m = o / 16, c = o % 16;
-    if (m >= M) continue;
-    float v[NREP];
-#pragma unroll
-    for (int j = 0; j < NREP; ++j) {
-      const int idx = (m * NREP + j) * 16 + c;
-      v[j] = ((red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx])) +
-             ((red[4][idx] + red[5][idx]) + (red[6][idx] + red[7][idx]));
-    }
-    if constexpr (Epi::kPaired) {
-      const int grp = blockIdx.x >> 1, half = blockIdx.x & 1;
-      epi.apply2(m, grp * 32 + half * 16 + c, v[0], v[NREP - 1], g);
-    } else {
-      if (col[0] + c < N) epi.apply(m, col[0] + c, v[0], g);
-    }
-  }
-}
-
 // Weight-streaming decode GEMM (M <= 32).  One workgroup = 16 output columns
 // (paired: 16 gate + 16 up packed columns) x one K split; wave w owns k-steps
 // w, w+8, ..., at most KSW of them, and issues ALL of its weight and
@@ -576,7 +483,7 @@ template <int MS, int KSW, class Epi>
 __global__ __launch_bounds__(512) void gemm_stream_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
     int64_t ldw, int M, int N, int K, int klen, int64_t a_goff, int64_t w_goff,
-    float* __restrict__ parts, Epi epi) {
+    float* __restrict__ parts, Epi epi, int packed) {
   constexpr int MR = MS / 16;
   constexpr int NREP = Epi::kPaired ? 2 : 1;
   __shared__ float red[8][MS * 16 * NREP];
@@ -603,8 +510,12 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
     const bool ok = k < kend;
 #pragma unroll
     for (int j = 0; j < NREP; ++j)
-      wb[u][j] = ok ? ld16(W + (int64_t)(col[j] + (lane & 15)) * ldw + k + koff)
-                    : zero;
+      if (packed)   // fragment-packed [N/16][K/32][64 lanes][8]: 1 KiB per load
+        wb[u][j] = ok ? ld16(W + (((int64_t)(col[j] >> 4) * (K >> 5) + (k >> 5)) * 64 + lane) * 8)
+                      : zero;
+      else
+        wb[u][j] = ok ? ld16(W + (int64_t)(col[j] + (lane & 15)) * ldw + k + koff)
+                      : zero;
   }
 #pragma unroll
   for (int u = 0; u < KSW; ++u) {
@@ -663,75 +574,6 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
   }
 }
 
-// Logits: the decode engine's main loop + soft-cap + per-workgroup argmax.
-template <int MS>
-__global__ __launch_bounds__(512) void logits_decode_kernel(
-    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
-    int64_t ldw, int M, int V, int K, float cap, u16* __restrict__ logits,
-    float* __restrict__ bval, int* __restrict__ bidx) {
-  constexpr int MR = MS / 16;
-  constexpr int U = 4;
-  __shared__ float red[8][MS * 16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16;
-  const int koff = 8 * (lane >> 4);
-  const int ksteps = K / 32;
-  f32x4 acc[MR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const uint4 zero = make_uint4(0, 0, 0, 0);
-  const u16* wrow = W + (int64_t)(n0 + (lane & 15)) * ldw + koff;
-  for (int ks0 = wave; ks0 < ksteps; ks0 += 8 * U) {
-    uint4 wb[U], xa[U][MR];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int ks = ks0 + 8 * u;
-      const bool ok = ks < ksteps;
-      wb[u] = ok ? ld16(wrow + ks * 32) : zero;
-#pragma unroll
-      for (int i = 0; i < MR; ++i) {
-        const int m = i * 16 + (lane & 15);
-        xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + ks * 32 + koff) : zero;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            __builtin_bit_cast(bf16x8, xa[u][i]), __builtin_bit_cast(bf16x8, wb[u]),
-            acc[i], 0, 0, 0);
-  }
-  const int rsub = (lane >> 4) * 4, csub = lane & 15;
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[wave][(i * 16 + rsub + r) * 16 + csub] = acc[i][r];
-  __syncthreads();
-  // thread o -> (row m, column c); 16 consecutive threads share a row
-  for (int o = threadIdx.x; o < MS * 16; o += 512) {
-    const int m = o / 16, c = o % 16;
-    float v = ((red[0][o] + red[1][o]) + (red[2][o] + red[3][o])) +
-              ((red[4][o] + red[5][o]) + (red[6][o] + red[7][o]));
-    float l = rbf(v);
-    if (cap > 0.0f) l = softcap(l, cap);
-    int idx = n0 + c;
-    const bool valid = m < M && idx < V;
-    if (valid && logits) logits[(int64_t)m * V + idx] = f2bf(l);
-    if (!valid) { l = -INFINITY; idx = 0x7fffffff; }
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) {
-      const float ov = __shfl_xor(l, off, 64);
-      const int oi = __shfl_xor(idx, off, 64);
-      if (ov > l || (ov == l && oi < idx)) { l = ov; idx = oi; }
-    }
-    if (c == 0 && m < M) {
-      bval[(int64_t)m * gridDim.x + blockIdx.x] = l;
-      bidx[(int64_t)m * gridDim.x + blockIdx.x] = idx;
-    }
-  }
-}
-
 // ---------------------------------------------------------- skinny engine
 
 // One block: 64 output columns x MS rows over one K split; 4 waves split the
@@ -740,7 +582,7 @@ template <int MS>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
     int64_t ldw, int M, int N, int K, int klen, float* __restrict__ part,
-    int64_t a_goff, int64_t w_goff) {
+    int64_t a_goff, int64_t w_goff, int packed) {
   constexpr int MR = MS / 16;
   constexpr int UNROLL = 2;
   __shared__ float red[4][MS * 64];
@@ -769,8 +611,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(
       const bool ok = k < kend;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        wb[u][j] = ok ? ld16(W + (int64_t)(n0 + j * 16 + (lane & 15)) * ldw + k + koff)
-                      : zero;
+        wb[u][j] = !ok ? zero
+                   : packed ? ld16(W + (((int64_t)((n0 >> 4) + j) * (K >> 5) + (k >> 5)) * 64 + lane) * 8)
+                            : ld16(W + (int64_t)(n0 + j * 16 + (lane & 15)) * ldw + k + koff);
 #pragma unroll
       for (int i = 0; i < MR; ++i) {
         const int m = i * 16 + (lane & 15);
@@ -908,23 +751,15 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(
 
 constexpr int kSkinnyMaxM = 64;
 
-// CADENCE_GEMM_LEGACY=1 selects the 128x128 register-staged tile kernel
-// (A/B comparisons in one binary).
-// Decode GEMM engine: split-K + ordered reduce (default, measured faster on
-// MI355X at B=32) or CADENCE_DECODE_ENGINE=fused for the single-pass
-// in-kernel-reduction engine.
-bool use_splitk_skinny() {
-  const char* e = getenv("CADENCE_DECODE_ENGINE");
-  return !(e && strncmp(e, "fused", 5) == 0);
-}
-
-// Weight-streaming plan for M <= 32 (CADENCE_DECODE_ENGINE=splitk disables):
-// k-steps per wave (KSW) and K splits so that one split is <= 8 * KSW steps.
+// Weight-streaming plan for M <= 32 (CADENCE_DECODE_ENGINE=splitk selects the
+// split-K skinny engine instead, for A/B runs): k-steps per wave (KSW) and K
+// splits so that one split is <= 8 * KSW steps.
 int stream_plan(int64_t M, int64_t K, int* ksw, int* splits) {
-  const char* e = getenv("CADENCE_DECODE_ENGINE");
-  if (M > 32 || K % 32 ||
-      (e && (strncmp(e, "splitk", 6) == 0 || strncmp(e, "fused", 5) == 0)))
-    return 0;
+  static const bool off = [] {
+    const char* e = getenv("CADENCE_DECODE_ENGINE");
+    return e && strncmp(e, "splitk", 6) == 0;
+  }();
+  if (M > 32 || K % 32 || off) return 0;
   const int64_t ks = K / 32;
   if (ks <= 8) { *ksw = 1; *splits = 1; }
   else if (ks <= 16) { *ksw = 2; *splits = 1; }
@@ -933,6 +768,8 @@ int stream_plan(int64_t M, int64_t K, int* ksw, int* splits) {
   return 1;
 }
 
+// CADENCE_GEMM_LEGACY=1 selects the 128x128 register-staged tile kernel
+// (A/B comparisons in one binary).
 bool use_legacy_tile() {
   const char* e = getenv("CADENCE_GEMM_LEGACY");
   return e && e[0] == '1';
@@ -961,6 +798,9 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                 int64_t w_goff, const Epi& epi, void* ws, int64_t ws_bytes,
                 hipStream_t st) {
   if (M <= 0) return 0;
+  // ldw == 0: W is fragment-packed (see cadence_kernels.h), decode engines only
+  const int packed = ldw == 0 ? 1 : 0;
+  if (packed && (M > kSkinnyMaxM || N % 16 || K % 32)) return (int)hipErrorInvalidValue;
   if (M > kSkinnyMaxM) {
     if (N % 64 || K % BK) return (int)hipErrorInvalidValue;
     if (use_legacy_tile() && N % 128 == 0) {
@@ -993,7 +833,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 #define CADENCE_STREAM(MS_, KSW_)                                               \
   hipLaunchKernelGGL((gemm_stream_kernel<MS_, KSW_, Epi>), grid, dim3(512), 0, st, \
                      A, lda, W, ldw, (int)M, (int)N, (int)K, klen, a_goff,      \
-                     w_goff, parts, epi)
+                     w_goff, parts, epi, packed)
     if (M <= 16) {
       if (ksw == 1) CADENCE_STREAM(16, 1);
       else if (ksw == 2) CADENCE_STREAM(16, 2);
@@ -1016,20 +856,6 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
     }
     return (int)hipGetLastError();
   }
-  if (!use_splitk_skinny()) {
-    const unsigned nblk = (unsigned)(Epi::kPaired ? N / 32 : N / 16);
-    dim3 grid(nblk, (unsigned)groups);
-    if (M <= 16)
-      hipLaunchKernelGGL((gemm_decode_kernel<16, Epi>), grid, dim3(512), 0, st, A,
-                         lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
-    else if (M <= 32)
-      hipLaunchKernelGGL((gemm_decode_kernel<32, Epi>), grid, dim3(512), 0, st, A,
-                         lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
-    else
-      hipLaunchKernelGGL((gemm_decode_kernel<64, Epi>), grid, dim3(512), 0, st, A,
-                         lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
-    return (int)hipGetLastError();
-  }
   const int splits = skinny_splits(N, K, groups);
   const int64_t klen = skinny_klen(K, splits);
   const int64_t need = (int64_t)splits * groups * M * N * 4;
@@ -1038,13 +864,16 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
   dim3 grid((unsigned)(N / 64), (unsigned)splits, (unsigned)groups);
   if (M <= 16)
     hipLaunchKernelGGL((gemm_skinny_kernel<16>), grid, dim3(256), 0, st, A, lda, W,
-                       ldw, (int)M, (int)N, (int)K, (int)klen, part, a_goff, w_goff);
+                       ldw, (int)M, (int)N, (int)K, (int)klen, part, a_goff, w_goff,
+                       packed);
   else if (M <= 32)
     hipLaunchKernelGGL((gemm_skinny_kernel<32>), grid, dim3(256), 0, st, A, lda, W,
-                       ldw, (int)M, (int)N, (int)K, (int)klen, part, a_goff, w_goff);
+                       ldw, (int)M, (int)N, (int)K, (int)klen, part, a_goff, w_goff,
+                       packed);
   else
     hipLaunchKernelGGL((gemm_skinny_kernel<64>), grid, dim3(256), 0, st, A, lda, W,
-                       ldw, (int)M, (int)N, (int)K, (int)klen, part, a_goff, w_goff);
+                       ldw, (int)M, (int)N, (int)K, (int)klen, part, a_goff, w_goff,
+                       packed);
   int64_t outs = M * N;
   int rblocks = (int)((outs + 255) / 256);
   if (rblocks > 4096) rblocks = 4096;
@@ -1057,14 +886,14 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 1; }
+int cadence_abi_version(void) { return 3; }
 
 int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
                                      int64_t groups) {
   int ksw = 0, ss = 0;
   if (M > 0 && stream_plan(M, K, &ksw, &ss))
     return ss > 1 ? (int64_t)ss * groups * M * N * 4 : 0;
-  if (M > kSkinnyMaxM || M <= 0 || !use_splitk_skinny()) return 0;
+  if (M > kSkinnyMaxM || M <= 0) return 0;
   const int splits = skinny_splits(N, K, groups);
   return (int64_t)splits * groups * M * N * 4;
 }
@@ -1085,26 +914,26 @@ int cadence_gemm_linear(const void* A, int64_t lda, const void* W, int64_t ldw,
 }
 
 int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
-                            const void* bias_gate, const void* bias_up,
-                            void* out, int64_t ldo, int64_t M, int64_t F,
-                            int64_t K, void* workspace, int64_t ws_bytes,
-                            void* stream) {
-  if (F % 64) return (int)hipErrorInvalidValue;
+                            int64_t ldw, const void* bias_gate,
+                            const void* bias_up, void* out, int64_t ldo,
+                            int64_t M, int64_t F, int64_t K, void* workspace,
+                            int64_t ws_bytes, void* stream) {
+  if (F % 64 || (ldw != 0 && ldw < K)) return (int)hipErrorInvalidValue;
   EpiGatedGelu epi{static_cast<u16*>(out), ldo,
                    static_cast<const u16*>(bias_gate),
                    static_cast<const u16*>(bias_up)};
   return launch_gemm(static_cast<const u16*>(A), lda,
-                     static_cast<const u16*>(Wpacked), K, M, 2 * F, K, 1, 0, 0,
+                     static_cast<const u16*>(Wpacked), ldw, M, 2 * F, K, 1, 0, 0,
                      epi, workspace, ws_bytes, static_cast<hipStream_t>(stream));
 }
 
 int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
-                        const void* bias_x, const void* bias_a,
+                        int64_t ldw, const void* bias_x, const void* bias_a,
                         const void* softplus_a, const int32_t* segment_pos,
                         void* a_out, void* nx_out, int64_t ldo, int64_t M,
                         int64_t heads, int64_t bw, void* workspace,
                         int64_t ws_bytes, void* stream) {
-  if (bw % 64) return (int)hipErrorInvalidValue;
+  if (bw % 64 || (ldw != 0 && ldw != bw)) return (int)hipErrorInvalidValue;
   EpiRglruGates epi{static_cast<const u16*>(X), ldx,
                     static_cast<const u16*>(bias_x),
                     static_cast<const u16*>(bias_a),
@@ -1112,7 +941,7 @@ int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
                     static_cast<u16*>(a_out), static_cast<u16*>(nx_out), ldo,
                     (int)bw};
   return launch_gemm(static_cast<const u16*>(X), ldx,
-                     static_cast<const u16*>(Wpacked), bw, M, 2 * bw, bw, heads,
+                     static_cast<const u16*>(Wpacked), ldw, M, 2 * bw, bw, heads,
                      bw, 2 * bw * bw, epi, workspace, ws_bytes,
                      static_cast<hipStream_t>(stream));
 }
@@ -1143,43 +972,21 @@ int cadence_gemm_patch_embed(const void* patches, int64_t ldp, const void* W,
 
 int64_t cadence_logits_scratch_bytes(int64_t M, int64_t V, int64_t D) {
   const int splits = skinny_splits(V, D, 1);
-  const int64_t nblk = (V + 15) / 16;   // >= the split-K path's V / 256 blocks
+  const int64_t nblk = (V + 255) / 256;
   return (int64_t)splits * M * V * 4 + M * nblk * 8 + 256;
 }
 
 int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
-                          int64_t M, int64_t V, int64_t D, float soft_cap,
-                          void* logits_out, int32_t* next_token,
+                          int64_t lde, int64_t M, int64_t V, int64_t D,
+                          float soft_cap, void* logits_out, int32_t* next_token,
                           void* scratch, int64_t scratch_bytes, void* stream) {
   if (M <= 0) return 0;
-  if (M > kSkinnyMaxM || V % 64 || D % 32) return (int)hipErrorInvalidValue;
+  if (M > kSkinnyMaxM || V % 64 || D % 32 || (lde != 0 && lde < D))
+    return (int)hipErrorInvalidValue;
   if (scratch_bytes < cadence_logits_scratch_bytes(M, V, D))
     return (int)hipErrorInvalidValue;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (!use_splitk_skinny()) {
-    const int64_t nblk = V / 16;
-    float* bval = static_cast<float*>(scratch);
-    int* bidx = reinterpret_cast<int*>(bval + M * nblk);
-    const u16* A = static_cast<const u16*>(X);
-    const u16* W = static_cast<const u16*>(E);
-    u16* lo = static_cast<u16*>(logits_out);
-    if (M <= 16)
-      hipLaunchKernelGGL(logits_decode_kernel<16>, dim3((unsigned)nblk), dim3(512), 0,
-                         st, A, ldx, W, D, (int)M, (int)V, (int)D, soft_cap, lo,
-                         bval, bidx);
-    else if (M <= 32)
-      hipLaunchKernelGGL(logits_decode_kernel<32>, dim3((unsigned)nblk), dim3(512), 0,
-                         st, A, ldx, W, D, (int)M, (int)V, (int)D, soft_cap, lo,
-                         bval, bidx);
-    else
-      hipLaunchKernelGGL(logits_decode_kernel<64>, dim3((unsigned)nblk), dim3(512), 0,
-                         st, A, ldx, W, D, (int)M, (int)V, (int)D, soft_cap, lo,
-                         bval, bidx);
-    if (next_token)
-      hipLaunchKernelGGL(argmax_final_kernel, dim3((unsigned)M), dim3(256), 0, st,
-                         bval, bidx, (int)nblk, next_token);
-    return (int)hipGetLastError();
-  }
+  const int packed = lde == 0 ? 1 : 0;
   const int splits = skinny_splits(V, D, 1);
   const int64_t klen = skinny_klen(D, splits);
   float* part = static_cast<float*>(scratch);
@@ -1191,13 +998,16 @@ int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
   dim3 grid((unsigned)(V / 64), (unsigned)splits, 1);
   if (M <= 16)
     hipLaunchKernelGGL((gemm_skinny_kernel<16>), grid, dim3(256), 0, st, A, ldx, W,
-                       D, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0);
+                       lde, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0,
+                       packed);
   else if (M <= 32)
     hipLaunchKernelGGL((gemm_skinny_kernel<32>), grid, dim3(256), 0, st, A, ldx, W,
-                       D, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0);
+                       lde, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0,
+                       packed);
   else
     hipLaunchKernelGGL((gemm_skinny_kernel<64>), grid, dim3(256), 0, st, A, ldx, W,
-                       D, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0);
+                       lde, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0,
+                       packed);
   hipLaunchKernelGGL(logits_reduce_kernel, dim3((unsigned)nblk, (unsigned)M),
                      dim3(256), 0, st, part, splits, (int)M, (int)V, soft_cap,
                      static_cast<u16*>(logits_out), bval, bidx);
@@ -1207,14 +1017,14 @@ int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
   return (int)hipGetLastError();
 }
 
-int cadence_gemm_logits(const void* X, int64_t ldx, const void* E, int64_t M,
-                        int64_t V, int64_t D, float soft_cap, void* out,
+int cadence_gemm_logits(const void* X, int64_t ldx, const void* E, int64_t lde,
+                        int64_t M, int64_t V, int64_t D, float soft_cap, void* out,
                         int64_t ldo, void* workspace, int64_t ws_bytes,
                         void* stream) {
   EpiLinear epi{static_cast<u16*>(out), ldo, nullptr, nullptr, 0,
                 soft_cap > 0.0f ? 2 : 0, RowMap{M > 0 ? M : 1, 0, 0}, soft_cap};
   return launch_gemm(static_cast<const u16*>(X), ldx, static_cast<const u16*>(E),
-                     D, M, V, D, 1, 0, 0, epi, workspace, ws_bytes,
+                     lde, M, V, D, 1, 0, 0, epi, workspace, ws_bytes,
                      static_cast<hipStream_t>(stream));
 }
 

@@ -9,7 +9,53 @@ namespace {
 // layers.py:73-78 on bf16 tensors: square (rounded), mean (fp32 sum,
 // rounded), + eps (rounded), rsqrt (rounded), x * r (rounded),
 // scale + 1 (rounded), product (rounded).
+// Rows up to 64 * 8 * RC wide stay in registers between the two passes:
+// x and scale are loaded once, up front (one memory round trip per row).
+template <int RC>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(
+    const u16* __restrict__ x, int64_t ldx, const u16* __restrict__ scale,
+    u16* __restrict__ out, int64_t ldo, int64_t rows, int width, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const u16* xr = x + row * ldx;
+  uint4 xv[RC], sv[RC];
+#pragma unroll
+  for (int i = 0; i < RC; ++i) {
+    const int c = min(lane * 8 + i * 512, width - 8);
+    xv[i] = ld16(xr + c);
+    sv[i] = ld16(scale + c);
+  }
+  float ss = 0.0f;
+#pragma unroll
+  for (int i = 0; i < RC; ++i) {
+    if (lane * 8 + i * 512 < width) {
+      float v[8];
+      unpack8(xv[i], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += rbf(v[j] * v[j]);
+    }
+  }
+  ss = wave_sum(ss);
+  const float var = rbf(ss / (float)width);
+  const float r = rbf(1.0f / sqrtf(rbf(var + eps)));
+  u16* orow = out + row * ldo;
+#pragma unroll
+  for (int i = 0; i < RC; ++i) {
+    const int c = lane * 8 + i * 512;
+    if (c < width) {
+      float v[8], sc[8];
+      unpack8(xv[i], v);
+      unpack8(sv[i], sc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bmul(bmul(v[j], r), badd(sc[j], 1.0f));
+      st16(orow + c, pack8(v));
+    }
+  }
+}
+
+// Wider rows: two passes over global memory.
+__global__ __launch_bounds__(256) void rmsnorm_wide_kernel(
     const u16* __restrict__ x, int64_t ldx, const u16* __restrict__ scale,
     u16* __restrict__ out, int64_t ldo, int64_t rows, int width, float eps) {
   const int lane = threadIdx.x & 63;
@@ -163,11 +209,20 @@ int cadence_rmsnorm(const void* x, int64_t ldx, const void* scale, void* out,
                     void* stream) {
   if (width % 8 || ldx % 8 || ldo % 8) return (int)hipErrorInvalidValue;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(rmsnorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256),
-                     0, static_cast<hipStream_t>(stream),
-                     static_cast<const u16*>(x), ldx,
-                     static_cast<const u16*>(scale), static_cast<u16*>(out), ldo,
-                     rows, (int)width, eps);
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const u16* xp = static_cast<const u16*>(x);
+  const u16* sp = static_cast<const u16*>(scale);
+  u16* op = static_cast<u16*>(out);
+  if (width <= 1024)
+    hipLaunchKernelGGL(rmsnorm_kernel<2>, grid, block, 0, st, xp, ldx, sp, op, ldo,
+                       rows, (int)width, eps);
+  else if (width <= 4096)
+    hipLaunchKernelGGL(rmsnorm_kernel<8>, grid, block, 0, st, xp, ldx, sp, op, ldo,
+                       rows, (int)width, eps);
+  else
+    hipLaunchKernelGGL(rmsnorm_wide_kernel, grid, block, 0, st, xp, ldx, sp, op, ldo,
+                       rows, (int)width, eps);
   return (int)hipGetLastError();
 }
 

@@ -82,25 +82,31 @@ __global__ __launch_bounds__(256) void conv1d_prefill_kernel(
 // Single-token decode: full = [state (TW-1 rows), x]; no document mask
 // (layers.py:478-483).  cache_out may alias cache_in (each thread reads its
 // 8 channels of every state row before writing them).
+template <int TW>
 __global__ __launch_bounds__(256) void conv1d_decode_kernel(
     const u16* __restrict__ x, int64_t ldx, const u16* __restrict__ w,
     const u16* __restrict__ bias, const u16* cache_in, u16* out, int64_t ldo,
-    u16* cache_out, int B, int E, int TW) {
+    u16* cache_out, int B, int E) {
   const int ch8 = E / 8;
   const int64_t total = (int64_t)B * ch8;
   for (int64_t idx = blockIdx.x * 256 + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * 256) {
     const int c = idx % ch8, b = idx / ch8;
     const int e0 = c * 8;
-    uint4 rows[8];  // TW <= 8
+    uint4 rows[TW], wr[TW];
+#pragma unroll
     for (int r = 0; r < TW - 1; ++r)
       rows[r] = ld16(cache_in + ((int64_t)b * (TW - 1) + r) * E + e0);
     rows[TW - 1] = ld16(x + (int64_t)b * ldx + e0);
+#pragma unroll
+    for (int r = 0; r < TW; ++r) wr[r] = ld16(w + (int64_t)r * E + e0);
+    const uint4 bq = ld16(bias + e0);
     float acc[8];
+#pragma unroll
     for (int s = 0; s < TW; ++s) {
       float xv[8], wv[8];
       unpack8(rows[TW - 1 - s], xv);
-      unpack8(ld16(w + (int64_t)(TW - 1 - s) * E + e0), wv);
+      unpack8(wr[TW - 1 - s], wv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float term = bmul(xv[i], wv[i]);
@@ -108,10 +114,11 @@ __global__ __launch_bounds__(256) void conv1d_decode_kernel(
       }
     }
     float bv[8];
-    unpack8(ld16(bias + e0), bv);
+    unpack8(bq, bv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = badd(acc[i], bv[i]);
     st16(out + (int64_t)b * ldo + e0, pack8(acc));
+#pragma unroll
     for (int r = 0; r < TW - 1; ++r)
       st16(cache_out + ((int64_t)b * (TW - 1) + r) * E + e0, rows[r + 1]);
   }
@@ -444,12 +451,20 @@ int cadence_conv1d(const void* x, int64_t ldx, const void* w, const void* b,
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (cache_in) {
     if (L != 1) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(conv1d_decode_kernel, dim3(grid_for(B * E / 8)), dim3(256),
-                       0, st, static_cast<const u16*>(x), ldx,
-                       static_cast<const u16*>(w), static_cast<const u16*>(b),
-                       static_cast<const u16*>(cache_in), static_cast<u16*>(out),
-                       ldo, static_cast<u16*>(cache_out), (int)B, (int)E,
-                       (int)temporal_width);
+    const dim3 grid(grid_for(B * E / 8)), block(256);
+    const u16* xp = static_cast<const u16*>(x);
+    const u16* wp = static_cast<const u16*>(w);
+    const u16* bp = static_cast<const u16*>(b);
+    const u16* ci = static_cast<const u16*>(cache_in);
+    u16* op = static_cast<u16*>(out);
+    u16* co = static_cast<u16*>(cache_out);
+    switch (temporal_width) {
+#define CADENCE_CONV_TW(T) \
+  case T: hipLaunchKernelGGL(conv1d_decode_kernel<T>, grid, block, 0, st, xp, ldx, wp, bp, ci, op, ldo, co, (int)B, (int)E); break;
+      CADENCE_CONV_TW(1) CADENCE_CONV_TW(2) CADENCE_CONV_TW(3) CADENCE_CONV_TW(4)
+      CADENCE_CONV_TW(5) CADENCE_CONV_TW(6) CADENCE_CONV_TW(7) CADENCE_CONV_TW(8)
+#undef CADENCE_CONV_TW
+    }
   } else {
     hipLaunchKernelGGL(conv1d_prefill_kernel, dim3(grid_for(B * L * E / 8)),
                        dim3(256), 0, st, static_cast<const u16*>(x), ldx,

@@ -14,6 +14,15 @@
  * layout; weights stored [K][N] by the reference, e.g. Einsum ffw_up, are
  * packed once by the host).
  *
+ * Decode weight layout: a weight leading dimension of 0 (ldw / lde == 0)
+ * means W is FRAGMENT-PACKED, accepted by the M <= 64 (decode) engines only:
+ *   Wp[((n / 16) * (K / 32) + k / 32) * 512 + l * 8 + e]
+ *       = W[16 * (n / 16) + l % 16][32 * (k / 32) + 8 * (l / 16) + e]
+ * for lane l in [0, 64), e in [0, 8) -- the MFMA 16x16x32 operand fragment
+ * order, so every wave load is 1 KiB contiguous and a workgroup's weight
+ * stream is one contiguous range.  Requires N % 16 == 0, K % 32 == 0;
+ * grouped launches pack each group separately.
+ *
  * The reference (`surakku/cadence-gemma`) has no native layer: each entry
  * point replaces a sequence of eager PyTorch ops (or timm ops) of the
  * reference Python path, cited per function.  The Python host
@@ -38,6 +47,7 @@ int cadence_abi_version(void);
 int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
                                      int64_t groups);
 
+
 /* ---- GEMMs with fused epilogues ---------------------------------------- */
 
 /* out[map(m), n] = act(A[m,:] . W[n,:] + bias[n]) (+ resid[map(m), n])
@@ -61,10 +71,10 @@ int cadence_gemm_linear(const void* A, int64_t lda, const void* W, int64_t ldw,
  * [32g, 32g + 32).  Replaces modules.py:754-756 (Einsum ffw_up + gelu + mul;
  * layers.py:726-729). */
 int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
-                            const void* bias_gate, const void* bias_up,
-                            void* out, int64_t ldo, int64_t M, int64_t F,
-                            int64_t K, void* workspace, int64_t ws_bytes,
-                            void* stream);
+                            int64_t ldw, const void* bias_gate,
+                            const void* bias_up, void* out, int64_t ldo,
+                            int64_t M, int64_t F, int64_t K, void* workspace,
+                            int64_t ws_bytes, void* stream);
 
 /* RG-LRU gates: both BlockDiagonalLinear layers of one RG-LRU as a grouped
  * GEMM (one group per head, K = block width) with the full gate chain fused
@@ -73,9 +83,10 @@ int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
  *   nx_out = x * sigmoid(gate_x) * (reset ? 1 : sqrt(1 - a^2))
  * with the bf16 rounding chain of the reference.  Wpacked is
  * [heads][2*bw][bw] (per 64-row group: 32 input-gate rows, 32 a-gate rows).
+ * ldw is bw (row-major) or 0 (fragment-packed per head).
  * Replaces layers.py:345-365 (+ 132-142 BlockDiagonalLinear, + 173). */
 int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
-                        const void* bias_x, const void* bias_a,
+                        int64_t ldw, const void* bias_x, const void* bias_a,
                         const void* softplus_a, const int32_t* segment_pos,
                         void* a_out, void* nx_out, int64_t ldo, int64_t M,
                         int64_t heads, int64_t bw, void* workspace,
@@ -106,16 +117,16 @@ int cadence_gemm_patch_embed(const void* patches, int64_t ldp, const void* W,
  * torch.argmax of examples/cadence_sampler.py:101-110.  `scratch` must hold
  * M * ceil(V / 64) * 8 bytes plus the split-K workspace. */
 int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
-                          int64_t M, int64_t V, int64_t D, float soft_cap,
-                          void* logits_out, int32_t* next_token,
+                          int64_t lde, int64_t M, int64_t V, int64_t D,
+                          float soft_cap, void* logits_out, int32_t* next_token,
                           void* scratch, int64_t scratch_bytes, void* stream);
 int64_t cadence_logits_scratch_bytes(int64_t M, int64_t V, int64_t D);
 
 /* All-position logits (Griffin.forward with return_logits=True,
  * griffin.py:216-221): out[m, v] = softcap(bf16(x[m] . E[v])) (cap 0 = off).
  * Uses the GEMM workspace rules of cadence_gemm_linear. */
-int cadence_gemm_logits(const void* X, int64_t ldx, const void* E, int64_t M,
-                        int64_t V, int64_t D, float soft_cap, void* out,
+int cadence_gemm_logits(const void* X, int64_t ldx, const void* E, int64_t lde,
+                        int64_t M, int64_t V, int64_t D, float soft_cap, void* out,
                         int64_t ldo, void* workspace, int64_t ws_bytes,
                         void* stream);
 
@@ -204,12 +215,19 @@ int cadence_kv_cache_fill(const void* k, const void* v,
 
 /* Single-token decode attention over the ring buffer + the new key, with the
  * slot positions of _compute_cache_mask (modules.py:155-185), then the
- * in-place cache update of _update_attention_cache (modules.py:210-218). */
+ * in-place cache update of _update_attention_cache (modules.py:210-218).
+ * With `workspace` (>= cadence_local_attention_decode_workspace_bytes) and
+ * `sems` (B zeroed int32 counters, left at zero) the window is split over 8
+ * workgroups per sequence and combined in-kernel in a fixed order; with
+ * either NULL one workgroup walks the whole window. */
+int64_t cadence_local_attention_decode_workspace_bytes(int64_t B, int64_t hd);
 int cadence_local_attention_decode(const void* q, const void* k_new,
                                    const void* v_new, void* cache_k,
                                    void* cache_v, int32_t* num_tokens,
                                    void* out, int64_t B, int64_t H,
-                                   int64_t hd, int64_t window, void* stream);
+                                   int64_t hd, int64_t window, void* workspace,
+                                   int64_t ws_bytes, int32_t* sems,
+                                   void* stream);
 
 /* ---- vision tower ---------------------------------------------------------- */
 

@@ -33,7 +33,7 @@ def test_host_contract_checks_without_gpu():
   lib = _lib.load()
   # workspace query is host-only arithmetic
   assert lib.cadence_gemm_workspace_bytes(4096, 2560, 2560, 1) == 0
-  assert lib.cadence_gemm_workspace_bytes(32, 2560, 2560, 1) > 0
+  assert lib.cadence_gemm_workspace_bytes(32, 2560, 7680, 1) > 0   # split K
   # contract violations are rejected before any launch (N % 64 != 0)
   assert lib.cadence_gemm_linear(None, 0, None, 0, None, None, 0, None, 0, 8,
                                  100, 64, 0, 8, 0, 0, None, 0, None) != 0

@@ -164,6 +164,47 @@ def test_gemm_linear(dev, m, n, k, act):
   assert_close_bf16(got, want.to(BF), rtol=1e-2, atol=1e-2, what="linear")
 
 
+@pytest.mark.parametrize("m,n,k", [(32, 2560, 2560), (32, 2560, 7680),
+                                   (5, 192, 96), (17, 4096, 2560)])
+def test_decode_packed_layout_bitwise(dev, m, n, k):
+  """The fragment-packed decode copy (ldw == 0) gives bit-identical results to
+  the row-major weight: same engine, same summation order."""
+  g = torch.Generator().manual_seed(11)
+  a = rnd(m, k, gen=g).to(dev)
+  w = rnd(n, k, scale=1 / math.sqrt(k), gen=g).to(dev)
+  bias = rnd(n, scale=0.1, gen=g).to(dev)
+  resid = rnd(m, n, gen=g).to(dev)
+  wp = ops.pack_decode(w)
+  o1 = torch.empty(m, n, dtype=BF, device=dev)
+  o2 = torch.empty(m, n, dtype=BF, device=dev)
+  ops.ops.gemm_linear_(a, w, bias, resid, o1, 0, m, 0, 0)
+  ops.ops.gemm_linear_(a, wp, bias, resid, o2, 0, m, 0, 0, True)
+  assert torch.equal(o1, o2)
+  assert torch.equal(ops.linear(a, w, bias, resid=resid), o1)   # auto-packed
+  if n % 128 == 0:       # gated kernel contract: F % 64 == 0
+    f = n // 2
+    bg, bu = rnd(f, scale=0.1, gen=g).to(dev), rnd(f, scale=0.1, gen=g).to(dev)
+    g1 = ops.ops.gated_gelu(a, w, bg, bu)
+    g2 = ops.ops.gated_gelu(a, wp, bg, bu, True)
+    assert torch.equal(g1, g2)
+  lg1, n1 = ops.ops.logits_argmax(a, w, 30.0, True)
+  lg2, n2 = ops.ops.logits_argmax(a, wp, 30.0, True, True)
+  assert torch.equal(lg1, lg2) and torch.equal(n1, n2)
+
+
+def test_decode_packed_rglru_gates_bitwise(dev):
+  g = torch.Generator().manual_seed(12)
+  h, bw, m = 10, 256, 32
+  x = rnd(m, h * bw, gen=g).to(dev)
+  w = rnd(h, 2 * bw, bw, scale=1 / 16, gen=g).to(dev)
+  bx, ba = rnd(h * bw, scale=0.3, gen=g).to(dev), rnd(h * bw, scale=0.3, gen=g).to(dev)
+  sp = torch.rand(h * bw, generator=g).to(BF).to(dev)
+  pos = torch.randint(0, 3, (m,), generator=g, dtype=torch.int32).to(dev)
+  a1, x1 = ops.ops.rglru_gates(x, w, bx, ba, sp, pos)
+  a2, x2 = ops.ops.rglru_gates(x, ops.pack_decode(w), bx, ba, sp, pos, True)
+  assert torch.equal(a1, a2) and torch.equal(x1, x2)
+
+
 def test_gemm_linear_residual_rowmap(dev):
   g = torch.Generator().manual_seed(6)
   m, n, k = 96, 256, 128
