@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -36,6 +36,8 @@ _SIGS: dict[str, list] = {
                                 I64, P],
     "cadence_rglru_gates": [P, I64, P, I64, P, P, P, P, P, P, I64, I64, I64, I64,
                             P, I64, P],
+    "cadence_rglru_step": [P, I64, P, I64, P, P, P, P, P, P, I64, P, I64, I64,
+                           I64, I64, P, I64, P],
     "cadence_gemm_vit_residual": [P, I64, P, I64, P, P, P, I64, I64, I64, I64,
                                   P, I64, P],
     "cadence_gemm_patch_embed": [P, I64, P, I64, P, P, P, I64, I64, I64, I64,

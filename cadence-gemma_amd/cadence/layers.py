@@ -186,6 +186,13 @@ class RGLRU(nn.Module):
     w, bx, ba, sp = self.packed()
     return ops.rglru_gates(x2d, w, bx, ba, sp, pos_flat)
 
+  def step_(self, x2d: torch.Tensor, pos_flat: torch.Tensor, h: torch.Tensor,
+            gate: torch.Tensor | None = None) -> torch.Tensor:
+    """One token per row (T = 1): gates + scan step fused, `h` updated in
+    place; returns bf16(h) [* gate]."""
+    w, bx, ba, sp = self.packed()
+    return ops.rglru_step_(x2d, w, bx, ba, sp, pos_flat, h, gate)
+
   def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,
               cache: torch.Tensor | None = None, return_cache: bool = True):
     b, t, e = x.shape

@@ -193,8 +193,8 @@ class RecurrentBlock(nn.Module):
       # decode: conv / RG-LRU states are advanced in place by the kernels
       conv_out = ops.ops.conv1d_step_(x_br, self.conv_1d.w, self.conv_1d.b,
                                       cache.conv1d_state)
-      a, nx = self.rg_lru.gates(conv_out, pos.view(-1))
-      gated = ops.ops.rnn_scan_(nx, a, cache.rg_lru_state, y_br, b, t)
+      gated = self.rg_lru.step_(conv_out, pos.view(-1), cache.rg_lru_state,
+                                y_br)
       out = ops.linear(gated, self.linear_out.weight, self.linear_out.bias,
                        resid=resid2d)
       return out, cache

@@ -229,6 +229,29 @@ def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos,
   return a, nx
 
 
+@_reg("rglru_step_(Tensor x, Tensor w_packed, Tensor bias_x, Tensor bias_a, "
+      "Tensor softplus_a, Tensor segment_pos, Tensor(a!) h, Tensor? gate, "
+      "bool decode_layout=False) -> Tensor")
+def _rglru_step(x, w_packed, bias_x, bias_a, softplus_a, segment_pos, h, gate,
+                decode_layout=False):
+  """Gate GEMM + chain + the T == 1 scan step; `h` [M, E] fp32 in place."""
+  ldx = _mat(x, "x")
+  M, E = x.shape
+  H, two_bw, bw = w_packed.shape
+  _need(two_bw == 2 * bw and H * bw == E, "w_packed shape")
+  _need(segment_pos.dtype == _I32 and segment_pos.numel() == M, "segment_pos")
+  _need(h.dtype == _F32 and h.is_contiguous() and tuple(h.shape) == (M, E),
+        "h: [M, E] fp32 contiguous")
+  ldg = _mat(gate, "gate") if gate is not None else 0
+  y = torch.empty(M, E, dtype=_BF16, device=x.device)
+  ws, nws = _ws(M, 2 * bw, bw, H, x)
+  _lib.check(_lib.load().cadence_rglru_step(
+      _p(x), ldx, _p(w_packed), 0 if decode_layout else bw, _p(bias_x),
+      _p(bias_a), _p(softplus_a), _p(segment_pos.contiguous()), _p(h),
+      _p(gate), ldg, _p(y), E, M, H, bw, _p(ws), nws, _s(x)), "rglru_step")
+  return y
+
+
 @_reg("vit_residual_(Tensor a, Tensor w, Tensor bias, Tensor? gamma, "
       "Tensor(a!) resid) -> ()")
 def _vit_residual(a, w, bias, gamma, resid):
@@ -595,6 +618,15 @@ def rglru_gates(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat):
   if wd is not None:
     return ops.rglru_gates(x2d, wd, bias_x, bias_a, softplus_a, pos_flat, True)
   return ops.rglru_gates(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat)
+
+
+def rglru_step_(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat, h, gate):
+  wd = decode_weight(w_packed) if x2d.shape[0] <= 32 else None
+  if wd is not None:
+    return ops.rglru_step_(x2d, wd, bias_x, bias_a, softplus_a, pos_flat, h,
+                           gate, True)
+  return ops.rglru_step_(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat, h,
+                         gate)
 
 
 def logits_argmax(x2d, embedding, soft_cap, return_logits):

@@ -122,6 +122,12 @@ struct EpiRglruGates {
   const int32_t* segpos;             // [M]
   u16* a_out; u16* nx_out; int64_t ldo;
   int bw;                            // block width (256)
+  // Single-token step (decode): when h != nullptr the scan step is fused
+  // here instead of writing (a, nx): h = a*h + nx (fp32, layers.py:175-182),
+  // y = bf16(h) [* gate], state updated in place.
+  float* h; int64_t ldh;
+  const u16* gate; int64_t ldg;
+  u16* y_out; int64_t ldy;
   CADENCE_DEV void apply2(int64_t m, int j, float accx, float acca, int g) const {
     const int e = g * bw + j;
     const float gx = rbf(sigmoidf_(badd(rbf(accx), bf2f(bias_x[e]))));
@@ -132,8 +138,19 @@ struct EpiRglruGates {
     const float gated = bmul(bf2f(x[m * ldx + e]), gx);
     const bool reset = segpos[m] == 0;
     const float mult = reset ? 1.0f : rbf(sqrtf(rbf(1.0f - a_sq)));
-    a_out[m * ldo + e] = f2bf(reset ? 0.0f : a);
-    nx_out[m * ldo + e] = f2bf(bmul(gated, mult));
+    const float av = reset ? 0.0f : a;
+    const float nx = bmul(gated, mult);
+    if (h) {
+      float* hp = h + m * ldh + e;
+      const float hn = add_rn(mul_rn(av, *hp), nx);
+      *hp = hn;
+      float y = rbf(hn);
+      if (gate) y = bmul(y, bf2f(gate[m * ldg + e]));
+      y_out[m * ldy + e] = f2bf(y);
+      return;
+    }
+    a_out[m * ldo + e] = f2bf(av);
+    nx_out[m * ldo + e] = f2bf(nx);
   }
 };
 
@@ -886,7 +903,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 3; }
+int cadence_abi_version(void) { return 4; }
 
 int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
                                      int64_t groups) {
@@ -939,7 +956,28 @@ int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
                     static_cast<const u16*>(bias_a),
                     static_cast<const u16*>(softplus_a), segment_pos,
                     static_cast<u16*>(a_out), static_cast<u16*>(nx_out), ldo,
-                    (int)bw};
+                    (int)bw, nullptr, 0, nullptr, 0, nullptr, 0};
+  return launch_gemm(static_cast<const u16*>(X), ldx,
+                     static_cast<const u16*>(Wpacked), ldw, M, 2 * bw, bw, heads,
+                     bw, 2 * bw * bw, epi, workspace, ws_bytes,
+                     static_cast<hipStream_t>(stream));
+}
+
+int cadence_rglru_step(const void* X, int64_t ldx, const void* Wpacked,
+                       int64_t ldw, const void* bias_x, const void* bias_a,
+                       const void* softplus_a, const int32_t* segment_pos,
+                       float* h, const void* gate, int64_t ldg, void* y_out,
+                       int64_t ldy, int64_t M, int64_t heads, int64_t bw,
+                       void* workspace, int64_t ws_bytes, void* stream) {
+  if (bw % 64 || (ldw != 0 && ldw != bw) || !h || !y_out)
+    return (int)hipErrorInvalidValue;
+  EpiRglruGates epi{static_cast<const u16*>(X), ldx,
+                    static_cast<const u16*>(bias_x),
+                    static_cast<const u16*>(bias_a),
+                    static_cast<const u16*>(softplus_a), segment_pos,
+                    nullptr, nullptr, 0, (int)bw, h, heads * bw,
+                    static_cast<const u16*>(gate), ldg, static_cast<u16*>(y_out),
+                    ldy};
   return launch_gemm(static_cast<const u16*>(X), ldx,
                      static_cast<const u16*>(Wpacked), ldw, M, 2 * bw, bw, heads,
                      bw, 2 * bw * bw, epi, workspace, ws_bytes,

@@ -92,6 +92,18 @@ int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
                         int64_t heads, int64_t bw, void* workspace,
                         int64_t ws_bytes, void* stream);
 
+/* Single-token RG-LRU step (decode, T = 1): the gate GEMM + chain of
+ * cadence_rglru_gates with the scan step of rnn_scan's T == 1 branch fused
+ * into the epilogue (layers.py:175-182, modules.py:652):
+ *   h[m, e] = a * h[m, e] + nx (fp32, in place);  y = bf16(h) [* gate]
+ * h is [M][heads * bw] fp32; gate (may be NULL) is the linear_y branch. */
+int cadence_rglru_step(const void* X, int64_t ldx, const void* Wpacked,
+                       int64_t ldw, const void* bias_x, const void* bias_a,
+                       const void* softplus_a, const int32_t* segment_pos,
+                       float* h, const void* gate, int64_t ldg, void* y_out,
+                       int64_t ldy, int64_t M, int64_t heads, int64_t bw,
+                       void* workspace, int64_t ws_bytes, void* stream);
+
 /* ViT residual branch (fp32 residual stream, in place):
  *   resid[m, n] += gamma[n] * (A[m,:] . W[n,:] + bias[n])   (gamma may be 0)
  * Replaces timm Block `x + ls(attn.proj(.))` / `x + ls(mlp.fc2(.))`. */

@@ -205,6 +205,31 @@ def test_decode_packed_rglru_gates_bitwise(dev):
   assert torch.equal(a1, a2) and torch.equal(x1, x2)
 
 
+@pytest.mark.parametrize("packed", [False, True])
+def test_rglru_step_matches_gates_then_scan(dev, packed):
+  """Fused decode step == gate chain then rnn_scan's T == 1 branch, bitwise,
+  with resets, a non-zero state and the y gate (row stride 2E)."""
+  g = torch.Generator().manual_seed(13)
+  h_, bw, m = 10, 256, 32
+  e = h_ * bw
+  x = rnd(m, e, gen=g).to(dev)
+  yx = rnd(m, 2 * e, gen=g).to(dev)
+  gate = yx[:, :e]
+  w = rnd(h_, 2 * bw, bw, scale=1 / 16, gen=g).to(dev)
+  bx, ba = rnd(e, scale=0.3, gen=g).to(dev), rnd(e, scale=0.3, gen=g).to(dev)
+  sp = torch.rand(e, generator=g).to(BF).to(dev)
+  pos = torch.randint(0, 3, (m,), generator=g, dtype=torch.int32).to(dev)
+  h0 = torch.randn(m, e, generator=g).to(dev)
+  a, nx = ops.ops.rglru_gates(x, w, bx, ba, sp, pos)
+  h_ref = h0.clone()
+  want = ops.ops.rnn_scan_(nx, a, h_ref, gate, m, 1)
+  h = h0.clone()
+  wk = ops.pack_decode(w) if packed else w
+  got = ops.ops.rglru_step_(x, wk, bx, ba, sp, pos, h, gate, packed)
+  assert torch.equal(got, want)
+  assert torch.equal(h, h_ref)
+
+
 def test_gemm_linear_residual_rowmap(dev):
   g = torch.Generator().manual_seed(6)
   m, n, k = 96, 256, 128
