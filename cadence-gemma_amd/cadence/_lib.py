@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -36,6 +36,9 @@ _SIGS: dict[str, list] = {
                                 I64, P],
     "cadence_rglru_gates": [P, I64, P, I64, P, P, P, P, P, P, I64, I64, I64, I64,
                             P, I64, P],
+    "cadence_gemm_rmsnorm_workspace_bytes": [I64, I64, I64],
+    "cadence_gemm_linear_rmsnorm": [P, I64, P, I64, P, P, I64, P, I64, I64, I64,
+                                    I64, P, F32, P, I64, P, I64, P],
     "cadence_rglru_step": [P, I64, P, I64, P, P, P, P, P, P, I64, P, I64, I64,
                            I64, I64, P, I64, P],
     "cadence_gemm_vit_residual": [P, I64, P, I64, P, P, P, I64, I64, I64, I64,
@@ -70,6 +73,7 @@ _SIGS: dict[str, list] = {
 _RESTYPE = {
     "cadence_gemm_workspace_bytes": I64,
     "cadence_local_attention_decode_workspace_bytes": I64,
+    "cadence_gemm_rmsnorm_workspace_bytes": I64,
     "cadence_logits_scratch_bytes": I64,
 }
 

@@ -106,14 +106,23 @@ class Griffin(nn.Module):
     return x, pos, t
 
   def run_blocks(self, x, pos, b, length, cache, return_cache,
-                 inplace_state=False):
+                 inplace_state=False, final_norm=False):
+    """Runs the residual blocks; each block's last GEMM also produces the
+    next norm's output.  Returns (x, final_norm(x) if final_norm else None,
+    cache)."""
     new_cache = {}
+    xn = None
+    n = len(self.blocks)
     for i, block in enumerate(self.blocks):
       name = f"blocks.{i}"
-      x, new_cache[name] = block.fused(
+      nxt = (self.blocks[i + 1].temporal_pre_norm if i + 1 < n else
+             (self.final_norm if final_norm else None))
+      x, xn, new_cache[name] = block.fused(
           x, pos, b, length, None if cache is None else cache[name],
-          return_cache, inplace_state)
-    return x, new_cache
+          return_cache, inplace_state, xn, nxt)
+    if final_norm and xn is None:
+      xn = ops.rmsnorm(x, self.final_norm.scale, self.final_norm.eps)
+    return x, xn, new_cache
 
   # ------------------------------------------------------------------ API
 
@@ -130,12 +139,12 @@ class Griffin(nn.Module):
       segment_pos = segment_pos[None, :]
     b = tokens.shape[0]
     x, pos, length = self.embed_inputs(tokens, segment_pos, images, img_path)
-    x, new_cache = self.run_blocks(x, pos, b, length, cache, return_cache)
+    x, xn, new_cache = self.run_blocks(x, pos, b, length, cache, return_cache,
+                                       final_norm=return_logits)
     if not return_cache:
       new_cache = None
     if not return_logits:
       return None, new_cache
-    xn = ops.rmsnorm(x, self.final_norm.scale, self.final_norm.eps)
     logits = ops.gemm_logits(xn, self.embedder.input_embedding,
                              float(self.config.logits_soft_cap or 0.0))
     return logits.view(b, length, -1), new_cache
@@ -153,8 +162,8 @@ class Griffin(nn.Module):
     b = tokens.shape[0]
     x, pos, _ = self.embed_inputs(tokens.reshape(b, 1),
                                   segment_pos.reshape(b, 1))
-    x, new_cache = self.run_blocks(x, pos, b, 1, cache, True, inplace)
-    xn = ops.rmsnorm(x, self.final_norm.scale, self.final_norm.eps)
+    x, xn, new_cache = self.run_blocks(x, pos, b, 1, cache, True, inplace,
+                                       final_norm=True)
     logits, nxt = ops.logits_argmax(
         xn, self.embedder.input_embedding,
         float(self.config.logits_soft_cap or 0.0), return_logits)

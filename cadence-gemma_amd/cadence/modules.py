@@ -48,6 +48,14 @@ def gelu(x: torch.Tensor) -> torch.Tensor:
   return nn.functional.gelu(x, approximate="tanh")
 
 
+def _out_proj(x2d, lin: nn.Linear, resid2d, norm):
+  """Residual output projection, optionally fused with the RMSNorm that
+  consumes it (returns (out, norm(out) or None))."""
+  if norm is None:
+    return ops.linear(x2d, lin.weight, lin.bias, resid=resid2d), None
+  return ops.linear_rmsnorm(x2d, lin.weight, lin.bias, resid2d, norm)
+
+
 class LocalAttentionBlock(nn.Module):
   """Local multi-query attention (one shared key/value head)."""
 
@@ -90,8 +98,9 @@ class LocalAttentionBlock(nn.Module):
         lambda: torch.cat([self.proj_q.weight, self.proj_k.weight,
                            self.proj_v.weight]).contiguous())
 
-  def fused(self, xn2d, pos, b, t, cache, return_cache, resid2d):
-    """Attention branch on normalised rows; returns (resid + out, cache)."""
+  def fused(self, xn2d, pos, b, t, cache, return_cache, resid2d, norm=None):
+    """Attention branch on normalised rows; returns (resid + out,
+    norm(resid + out) or None, cache)."""
     h, hd = self.num_heads, self.head_dim
     qkv = ops.linear(xn2d, self.qkv_weight())
     q, k, v = ops.ops.rope_qkv(qkv, pos.view(-1), h, hd,
@@ -111,9 +120,8 @@ class LocalAttentionBlock(nn.Module):
       enc = ops.ops.local_attention_decode_(q, k, v, cache.keys, cache.values,
                                             cache.num_tokens, h)
       new_cache = cache if return_cache else None
-    out = ops.linear(enc, self.proj_final.weight, self.proj_final.bias,
-                     resid=resid2d)
-    return out, new_cache
+    out, hn = _out_proj(enc, self.proj_final, resid2d, norm)
+    return out, hn, new_cache
 
   def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,
               cache: AttentionBlockCache | None = None,
@@ -121,7 +129,8 @@ class LocalAttentionBlock(nn.Module):
     b, t, d = x.shape
     pos = positions_2d(segment_pos, b, t)
     zero = torch.zeros(b * t, d, dtype=x.dtype, device=x.device)
-    out, new_cache = self.fused(_flat(x), pos, b, t, cache, return_cache, zero)
+    out, _, new_cache = self.fused(_flat(x), pos, b, t, cache, return_cache,
+                                   zero)
     return out.view(b, t, d), new_cache
 
   @classmethod
@@ -182,7 +191,7 @@ class RecurrentBlock(nn.Module):
         torch.cat([self.linear_y.bias, self.linear_x.bias]).contiguous()))
 
   def fused(self, xn2d, pos, b, t, cache, return_cache, resid2d,
-            inplace_state: bool = False):
+            inplace_state: bool = False, norm=None):
     e = self.lru_width
     w, bias = self.yx_weight()
     yx = ops.linear(xn2d, w, bias)                       # [M, 2E]: y | x
@@ -195,23 +204,22 @@ class RecurrentBlock(nn.Module):
                                       cache.conv1d_state)
       gated = self.rg_lru.step_(conv_out, pos.view(-1), cache.rg_lru_state,
                                 y_br)
-      out = ops.linear(gated, self.linear_out.weight, self.linear_out.bias,
-                       resid=resid2d)
-      return out, cache
+      out, hn = _out_proj(gated, self.linear_out, resid2d, norm)
+      return out, hn, cache
     conv_out, conv_state = self.conv_1d.apply2d(
         x_br, pos, None if cache is None else cache.conv1d_state, b, t)
     a, nx = self.rg_lru.gates(conv_out, pos.view(-1))
     h0 = None if cache is None else cache.rg_lru_state
     gated, h_last = ops.ops.rnn_scan(nx, a, None, h0, y_br, b, t)
-    out = ops.linear(gated, self.linear_out.weight, self.linear_out.bias,
-                     resid=resid2d)
+    out, hn = _out_proj(gated, self.linear_out, resid2d, norm)
     if not return_cache:
-      return out, None
+      return out, hn, None
     if inplace_state and cache is not None:
       cache.rg_lru_state.copy_(h_last)
       cache.conv1d_state.copy_(conv_state)
-      return out, cache
-    return out, RecurrentBlockCache(rg_lru_state=h_last, conv1d_state=conv_state)
+      return out, hn, cache
+    return out, hn, RecurrentBlockCache(rg_lru_state=h_last,
+                                        conv1d_state=conv_state)
 
   def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,
               cache: RecurrentBlockCache | None = None,
@@ -219,7 +227,8 @@ class RecurrentBlock(nn.Module):
     b, t, d = x.shape
     pos = positions_2d(segment_pos, b, t)
     zero = torch.zeros(b * t, d, dtype=x.dtype, device=x.device)
-    out, new_cache = self.fused(_flat(x), pos, b, t, cache, return_cache, zero)
+    out, _, new_cache = self.fused(_flat(x), pos, b, t, cache, return_cache,
+                                   zero)
     return out.view(b, t, d), new_cache
 
   @classmethod
@@ -256,15 +265,15 @@ class MLPBlock(nn.Module):
         self.final_w_init_variance_scale / self.expanded_width))
     nn.init.zeros_(self.ffw_down.bias)
 
-  def fused(self, xn2d, resid2d):
+  def fused(self, xn2d, resid2d, norm=None):
+    """resid + MLP(xn); with `norm` also returns norm(that) (else None)."""
     w, bg, bu = self.ffw_up.gated_packed()
     act = ops.gated_gelu(xn2d, w, bg, bu)
-    return ops.linear(act, self.ffw_down.weight, self.ffw_down.bias,
-                      resid=resid2d)
+    return _out_proj(act, self.ffw_down, resid2d, norm)
 
   def forward(self, x: torch.Tensor) -> torch.Tensor:
     zero = torch.zeros(_flat(x).shape, dtype=x.dtype, device=x.device)
-    return self.fused(_flat(x), zero).view(x.shape)
+    return self.fused(_flat(x), zero)[0].view(x.shape)
 
 
 class ResidualBlock(nn.Module):
@@ -312,26 +321,33 @@ class ResidualBlock(nn.Module):
     self.mlp_block.reset_parameters()
 
   def fused(self, x2d, pos, b, t, cache, return_cache,
-            inplace_state: bool = False):
-    """One residual block on [B*T, D] rows; returns (out rows, cache)."""
-    xn = ops.rmsnorm(x2d, self.temporal_pre_norm.scale,
-                     self.temporal_pre_norm.eps)
+            inplace_state: bool = False, xn=None, next_norm=None):
+    """One residual block on [B*T, D] rows.
+
+    `xn` is temporal_pre_norm(x2d) when the previous block already produced
+    it; `next_norm` is the RMSNorm that consumes this block's output (the
+    next block's temporal_pre_norm or the final norm): each residual GEMM is
+    fused with the norm that follows it.  Returns (out, next_norm(out) or
+    None, cache)."""
+    if xn is None:
+      xn = ops.rmsnorm(x2d, self.temporal_pre_norm.scale,
+                       self.temporal_pre_norm.eps)
     if self.temporal_block_type == common.TemporalBlockType.RECURRENT:
-      resid, new_cache = self.recurrent_block.fused(
-          xn, pos, b, t, cache, return_cache, x2d, inplace_state)
+      resid, hn, new_cache = self.recurrent_block.fused(
+          xn, pos, b, t, cache, return_cache, x2d, inplace_state,
+          self.channel_pre_norm)
     else:
-      resid, new_cache = self.attention_block.fused(
-          xn, pos, b, t, cache, return_cache, x2d)
-    hn = ops.rmsnorm(resid, self.channel_pre_norm.scale,
-                     self.channel_pre_norm.eps)
-    return self.mlp_block.fused(hn, resid), new_cache
+      resid, hn, new_cache = self.attention_block.fused(
+          xn, pos, b, t, cache, return_cache, x2d, self.channel_pre_norm)
+    out, out_norm = self.mlp_block.fused(hn, resid, next_norm)
+    return out, out_norm, new_cache
 
   def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,
               cache: ResidualBlockCache | None = None,
               return_cache: bool = True):
     b, t, d = x.shape
     pos = positions_2d(segment_pos, b, t)
-    out, new_cache = self.fused(_flat(x), pos, b, t, cache, return_cache)
+    out, _, new_cache = self.fused(_flat(x), pos, b, t, cache, return_cache)
     return out.view(b, t, d), new_cache
 
   @classmethod

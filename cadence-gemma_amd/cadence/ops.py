@@ -189,6 +189,29 @@ def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off,
   TIMER.stop(ev, "gemm_tile_kernel<EpiLinear>", 2.0 * M * N * K, a)
 
 
+@_reg("gemm_linear_rmsnorm(Tensor a, Tensor w, Tensor? bias, Tensor? resid, "
+      "Tensor scale, float eps, bool w_packed=False) -> (Tensor, Tensor)")
+def _gemm_linear_rmsnorm(a, w, bias, resid, scale, eps, w_packed=False):
+  """(out, rmsnorm(out)): out = a . w^T + bias (+ resid)."""
+  lda, ldw = _mat(a, "a"), _wld(w, w_packed, "w")
+  M, K = a.shape
+  N = w.shape[0]
+  ldr = _mat(resid, "resid") if resid is not None else 0
+  out = torch.empty(M, N, dtype=_BF16, device=a.device)
+  nout = torch.empty(M, N, dtype=_BF16, device=a.device)
+  lib = _lib.load()
+  nws = max(lib.cadence_gemm_rmsnorm_workspace_bytes(M, N, K),
+            lib.cadence_gemm_workspace_bytes(M, N, K, 1))
+  ws = torch.empty(nws, dtype=torch.uint8, device=a.device) if nws else None
+  ev = TIMER.start(a) if _tile(M) else None
+  _lib.check(lib.cadence_gemm_linear_rmsnorm(
+      _p(a), lda, _p(w), ldw, _p(bias), _p(resid), ldr, _p(out), N, M, N, K,
+      _p(scale), float(eps), _p(nout), N, _p(ws), nws, _s(a)),
+      "gemm_linear_rmsnorm")
+  TIMER.stop(ev, "gemm_tile_kernel<EpiLinear>", 2.0 * M * N * K, a)
+  return out, nout
+
+
 @_reg("gated_gelu(Tensor a, Tensor w_packed, Tensor bias_gate, "
       "Tensor bias_up, bool decode_layout=False) -> Tensor")
 def _gated_gelu(a, w_packed, bias_gate, bias_up, decode_layout=False):
@@ -603,6 +626,15 @@ def linear(x2d, w, bias=None, act=0, resid=None, out=None,
   else:
     ops.gemm_linear_(x2d, w, bias, resid, out, act, div, mul, off)
   return out
+
+
+def linear_rmsnorm(x2d, w, bias, resid, norm):
+  """(x2d . w^T + bias + resid, norm(that)) for a layers.RMSNorm `norm`."""
+  wd = decode_weight(w) if x2d.shape[0] <= 32 else None
+  if wd is not None:
+    return ops.gemm_linear_rmsnorm(x2d, wd, bias, resid, norm.scale, norm.eps,
+                                   True)
+  return ops.gemm_linear_rmsnorm(x2d, w, bias, resid, norm.scale, norm.eps)
 
 
 def gated_gelu(x2d, w_packed, bias_gate, bias_up):

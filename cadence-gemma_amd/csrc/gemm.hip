@@ -768,6 +768,80 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(
 
 constexpr int kSkinnyMaxM = 64;
 
+// Split-K finish of a residual GEMM that feeds an RMSNorm (decode): one
+// workgroup per output row.  out[m, :] = EpiLinear(sum_s part[s][m][:]) (bias,
+// rounding, + resid), then nout[m, :] = RMSNorm(out[m, :]) with the rounding
+// chain of rmsnorm_kernel (layers.py:73-78).  RC 8-column chunks per thread
+// stay in registers between the two passes.
+template <int RC, int S>
+__global__ __launch_bounds__(512) void reduce_rmsnorm_kernel(
+    const float* __restrict__ part, int M, int N, EpiLinear epi,
+    const u16* __restrict__ scale, float eps, u16* __restrict__ nout,
+    int64_t ldn) {
+  __shared__ float wsum[8];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const int64_t orow = epi.map(m);
+  // issue every load of the row first (S splits x RC chunks, resid, scale)
+  float4 pa[RC][S][2];
+  uint4 rq[RC], sq[RC];
+#pragma unroll
+  for (int c = 0; c < RC; ++c) {
+    const int n0 = min((tid + c * 512) * 8, N - 8);
+#pragma unroll
+    for (int sp = 0; sp < S; ++sp) {
+      const float4* src = reinterpret_cast<const float4*>(
+          part + ((int64_t)sp * M + m) * N + n0);
+      pa[c][sp][0] = src[0];
+      pa[c][sp][1] = src[1];
+    }
+    rq[c] = epi.resid ? ld16(epi.resid + orow * epi.ldr + n0) : make_uint4(0, 0, 0, 0);
+    sq[c] = ld16(scale + n0);
+  }
+  float o[RC][8];
+  float ss = 0.0f;
+#pragma unroll
+  for (int c = 0; c < RC; ++c) {
+    const int n0 = (tid + c * 512) * 8;
+    if (n0 < N) {
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sp = 0; sp < S; ++sp) {
+        const float4 a = pa[c][sp][0], b = pa[c][sp][1];
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+        v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+      float r[8];
+      unpack8(rq[c], r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float y = epi.value(m, n0 + i, v[i], 0);
+        if (epi.resid) y = badd(y, r[i]);
+        o[c][i] = y;
+        ss += rbf(y * y);
+      }
+      st16(epi.out + orow * epi.ldo + n0, pack8(o[c]));
+    }
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) wsum[tid >> 6] = ss;
+  __syncthreads();
+  ss = ((wsum[0] + wsum[1]) + (wsum[2] + wsum[3])) +
+       ((wsum[4] + wsum[5]) + (wsum[6] + wsum[7]));
+  const float var = rbf(ss / (float)N);
+  const float rs = rbf(1.0f / sqrtf(rbf(var + eps)));
+#pragma unroll
+  for (int c = 0; c < RC; ++c) {
+    const int n0 = (tid + c * 512) * 8;
+    if (n0 < N) {
+      float sc[8];
+      unpack8(sq[c], sc);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[c][i] = bmul(bmul(o[c][i], rs), badd(sc[i], 1.0f));
+      st16(nout + orow * ldn + n0, pack8(o[c]));
+    }
+  }
+}
+
 // Weight-streaming plan for M <= 32 (CADENCE_DECODE_ENGINE=splitk selects the
 // split-K skinny engine instead, for A/B runs): k-steps per wave (KSW) and K
 // splits so that one split is <= 8 * KSW steps.
@@ -809,6 +883,35 @@ int64_t skinny_klen(int64_t K, int splits) {
   return klen;
 }
 
+// Stream engine launch: `splits` K splits (raw fp32 partials to `parts`
+// [split][group][M][N] when > 1, else the epilogue runs in-kernel).
+template <class Epi>
+void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
+                   int64_t M, int64_t N, int64_t K, int64_t groups,
+                   int64_t a_goff, int64_t w_goff, const Epi& epi, int ksw,
+                   int splits, float* parts, int packed, hipStream_t st) {
+  const unsigned nblk = (unsigned)(Epi::kPaired ? N / 32 : N / 16);
+  const int64_t ks = K / 32;
+  const int klen = (int)((ks + splits - 1) / splits) * 32;
+  dim3 grid(nblk, (unsigned)splits, (unsigned)groups);
+#define CADENCE_STREAM(MS_, KSW_)                                               \
+  hipLaunchKernelGGL((gemm_stream_kernel<MS_, KSW_, Epi>), grid, dim3(512), 0, st, \
+                     A, lda, W, ldw, (int)M, (int)N, (int)K, klen, a_goff,      \
+                     w_goff, parts, epi, packed)
+  if (M <= 16) {
+    if (ksw == 1) CADENCE_STREAM(16, 1);
+    else if (ksw == 2) CADENCE_STREAM(16, 2);
+    else if (ksw == 4) CADENCE_STREAM(16, 4);
+    else CADENCE_STREAM(16, 10);
+  } else {
+    if (ksw == 1) CADENCE_STREAM(32, 1);
+    else if (ksw == 2) CADENCE_STREAM(32, 2);
+    else if (ksw == 4) CADENCE_STREAM(32, 4);
+    else CADENCE_STREAM(32, 10);
+  }
+#undef CADENCE_STREAM
+}
+
 template <class Epi>
 int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                 int64_t N, int64_t K, int64_t groups, int64_t a_goff,
@@ -837,32 +940,14 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
   if (N % 64 || K % 32) return (int)hipErrorInvalidValue;
   int ksw = 0, ssplits = 0;
   if (stream_plan(M, K, &ksw, &ssplits)) {
-    const unsigned nblk = (unsigned)(Epi::kPaired ? N / 32 : N / 16);
-    const int64_t ks = K / 32;
-    const int klen = (int)((ks + ssplits - 1) / ssplits) * 32;
     float* parts = nullptr;
     if (ssplits > 1) {
       const int64_t need = (int64_t)ssplits * groups * M * N * 4;
       if (!ws || ws_bytes < need) return (int)hipErrorInvalidValue;
       parts = static_cast<float*>(ws);
     }
-    dim3 grid(nblk, (unsigned)ssplits, (unsigned)groups);
-#define CADENCE_STREAM(MS_, KSW_)                                               \
-  hipLaunchKernelGGL((gemm_stream_kernel<MS_, KSW_, Epi>), grid, dim3(512), 0, st, \
-                     A, lda, W, ldw, (int)M, (int)N, (int)K, klen, a_goff,      \
-                     w_goff, parts, epi, packed)
-    if (M <= 16) {
-      if (ksw == 1) CADENCE_STREAM(16, 1);
-      else if (ksw == 2) CADENCE_STREAM(16, 2);
-      else if (ksw == 4) CADENCE_STREAM(16, 4);
-      else CADENCE_STREAM(16, 10);
-    } else {
-      if (ksw == 1) CADENCE_STREAM(32, 1);
-      else if (ksw == 2) CADENCE_STREAM(32, 2);
-      else if (ksw == 4) CADENCE_STREAM(32, 4);
-      else CADENCE_STREAM(32, 10);
-    }
-#undef CADENCE_STREAM
+    launch_stream(A, lda, W, ldw, M, N, K, groups, a_goff, w_goff, epi, ksw,
+                  ssplits, parts, packed, st);
     if (ssplits > 1) {
       int64_t outs = M * N;
       int rblocks = (int)((outs + 255) / 256);
@@ -903,7 +988,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 4; }
+int cadence_abi_version(void) { return 5; }
 
 int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
                                      int64_t groups) {
@@ -928,6 +1013,63 @@ int cadence_gemm_linear(const void* A, int64_t lda, const void* W, int64_t ldw,
   return launch_gemm(static_cast<const u16*>(A), lda, static_cast<const u16*>(W),
                      ldw, M, N, K, 1, 0, 0, epi, workspace, ws_bytes,
                      static_cast<hipStream_t>(stream));
+}
+
+int64_t cadence_gemm_rmsnorm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  int ksw = 0, ss = 0;
+  if (M <= 0 || N > 4096 || !stream_plan(M, K, &ksw, &ss) || ss < 2 || ss > 4)
+    return 0;
+  return (int64_t)ss * M * N * 4;
+}
+
+int cadence_gemm_linear_rmsnorm(const void* A, int64_t lda, const void* W,
+                                int64_t ldw, const void* bias,
+                                const void* resid, int64_t ld_resid, void* out,
+                                int64_t ldo, int64_t M, int64_t N, int64_t K,
+                                const void* norm_scale, float eps,
+                                void* norm_out, int64_t ld_norm,
+                                void* workspace, int64_t ws_bytes,
+                                void* stream) {
+  if (M <= 0) return 0;
+  if (N % 8 || ldo % 8 || ld_norm % 8 || (resid && ld_resid % 8))
+    return (int)hipErrorInvalidValue;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  EpiLinear epi{static_cast<u16*>(out), ldo, static_cast<const u16*>(bias),
+                static_cast<const u16*>(resid), ld_resid, 0,
+                RowMap{M, 0, 0}, 0.0f};
+  int ksw = 0, ss = 0;
+  if (N <= 4096 && N % 64 == 0 && stream_plan(M, K, &ksw, &ss) && ss >= 2 &&
+      ss <= 4) {
+    // decode GEMM that is split-K anyway (K > 2560): the row-owned reduce +
+    // residual + RMSNorm kernel replaces the split-K reduce and the norm.
+    // (Forcing a split on a single-pass GEMM measured slower.)
+    const int splits = ss;
+    const int64_t need = (int64_t)splits * M * N * 4;
+    if (!workspace || ws_bytes < need) return (int)hipErrorInvalidValue;
+    float* parts = static_cast<float*>(workspace);
+    launch_stream(static_cast<const u16*>(A), lda, static_cast<const u16*>(W), ldw,
+                  M, N, K, 1, 0, 0, epi, ksw, splits, parts, ldw == 0 ? 1 : 0, st);
+    const u16* sc = static_cast<const u16*>(norm_scale);
+    u16* no = static_cast<u16*>(norm_out);
+    const dim3 g((unsigned)M), b(512);
+#define CADENCE_RN(RC_, S_) \
+  hipLaunchKernelGGL((reduce_rmsnorm_kernel<RC_, S_>), g, b, 0, st, parts, (int)M, \
+                     (int)N, epi, sc, eps, no, ld_norm)
+    const bool one = N <= 4096;
+    switch (splits) {
+      case 2: if (one) CADENCE_RN(1, 2); else CADENCE_RN(2, 2); break;
+      case 3: if (one) CADENCE_RN(1, 3); else CADENCE_RN(2, 3); break;
+      case 4: if (one) CADENCE_RN(1, 4); else CADENCE_RN(2, 4); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+#undef CADENCE_RN
+    return (int)hipGetLastError();
+  }
+  const int rc = launch_gemm(static_cast<const u16*>(A), lda,
+                             static_cast<const u16*>(W), ldw, M, N, K, 1, 0, 0,
+                             epi, workspace, ws_bytes, st);
+  if (rc) return rc;
+  return cadence_rmsnorm(out, ldo, norm_scale, norm_out, ld_norm, M, N, eps, stream);
 }
 
 int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,

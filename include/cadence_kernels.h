@@ -65,6 +65,23 @@ int cadence_gemm_linear(const void* A, int64_t lda, const void* W, int64_t ldw,
                         int64_t row_off, void* workspace, int64_t ws_bytes,
                         void* stream);
 
+/* Residual GEMM that feeds an RMSNorm (the temporal-block output projection
+ * and ffw_down, each followed by the next norm; modules.py:908-913):
+ *   out = A . W^T + bias + resid          (as cadence_gemm_linear, act 0)
+ *   norm_out = RMSNorm(out; norm_scale)    (as cadence_rmsnorm)
+ * For M <= 32 the GEMM runs split-K and one row-owned kernel finishes the
+ * reduction, the residual and the norm (workspace:
+ * cadence_gemm_rmsnorm_workspace_bytes); otherwise GEMM + norm kernels. */
+int64_t cadence_gemm_rmsnorm_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int cadence_gemm_linear_rmsnorm(const void* A, int64_t lda, const void* W,
+                                int64_t ldw, const void* bias,
+                                const void* resid, int64_t ld_resid, void* out,
+                                int64_t ldo, int64_t M, int64_t N, int64_t K,
+                                const void* norm_scale, float eps,
+                                void* norm_out, int64_t ld_norm,
+                                void* workspace, int64_t ws_bytes,
+                                void* stream);
+
 /* MLP up-projection + gating: out[m, f] = gelu_tanh(x.Wg[f] + bg[f]) *
  * (x.Wu[f] + bu[f]).  W is the packed [2F][K] matrix in which every 64-row
  * group g holds 32 gate rows then the 32 up rows of features

@@ -230,6 +230,30 @@ def test_rglru_step_matches_gates_then_scan(dev, packed):
   assert torch.equal(h, h_ref)
 
 
+@pytest.mark.parametrize("m,n,k", [(32, 2560, 2560), (32, 2560, 7680),
+                                   (7, 512, 256), (100, 512, 256)])
+def test_gemm_linear_rmsnorm(dev, m, n, k):
+  """Residual GEMM fused with the following RMSNorm (decode: split-K finished
+  by the row-owned reduce+norm kernel) vs linear then rmsnorm."""
+  g = torch.Generator().manual_seed(14)
+  a = rnd(m, k, gen=g).to(dev)
+  w = rnd(n, k, scale=1 / math.sqrt(k), gen=g).to(dev)
+  bias = rnd(n, scale=0.1, gen=g).to(dev)
+  resid = rnd(m, n, gen=g).to(dev)
+  norm = cadence.layers.RMSNorm(n, device=dev, dtype=BF)
+  with torch.no_grad():
+    norm.scale.copy_(rnd(n, scale=0.2, gen=g))
+  out, nout = ops.linear_rmsnorm(a, w, bias, resid, norm)
+  ref = ops.linear(a, w, bias, resid=resid)
+  if m > 64:   # prefill: the same two kernels
+    assert torch.equal(out, ref)
+    assert torch.equal(nout, ops.rmsnorm(ref, norm.scale, norm.eps))
+  else:        # split-K order differs: bf16 tolerance
+    assert_close_bf16(out, ref.cpu(), rtol=1e-2, atol=2e-2, what="resid gemm")
+    want = R.rms_norm(out.cpu(), norm.scale.cpu())
+    assert_close_bf16(nout, want, rtol=2e-2, atol=2e-2, what="fused norm")
+
+
 def test_gemm_linear_residual_rowmap(dev):
   g = torch.Generator().manual_seed(6)
   m, n, k = 96, 256, 128
