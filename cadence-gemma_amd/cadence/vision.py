@@ -219,11 +219,35 @@ class VisionEncoder(nn.Module):
   def n_visual_tokens(self) -> int:
     return self.config.n_visual_tokens
 
+  def _side_stream(self, dev: torch.device) -> torch.cuda.Stream:
+    s = getattr(self, "_side", None)
+    if s is None or s.device != dev:
+      s = torch.cuda.Stream(device=dev)
+      self._side = s
+    return s
+
   def features_into(self, pixels: torch.Tensor, out2d: torch.Tensor):
-    """pixels [B,3,S,S] fp32 in [0,1] -> out2d [B*n_vis, 2176] bf16."""
+    """pixels [B,3,S,S] fp32 in [0,1] -> out2d [B*n_vis, 2176] bf16.
+
+    The two encoders are independent until their feature columns meet in
+    `out2d`, so SigLIP runs on a side stream beside DINO: the two towers'
+    GEMMs (132-160 output tiles each at bs=32, 224 px) fill the 256 CUs
+    together where either alone leaves ~40 % of them idle.  Not while a
+    graph is being captured (one stream there)."""
     n = self.config.blocks_run
+    if torch.cuda.is_current_stream_capturing() or not pixels.is_cuda:
+      self.dino.features_into(pixels, out2d, 0, n)
+      self.siglip.features_into(pixels, out2d, self.config.dino.width, n)
+      return
+    cur = torch.cuda.current_stream(pixels.device)
+    side = self._side_stream(pixels.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+      self.siglip.features_into(pixels, out2d, self.config.dino.width, n)
+    pixels.record_stream(side)
+    out2d.record_stream(side)
     self.dino.features_into(pixels, out2d, 0, n)
-    self.siglip.features_into(pixels, out2d, self.config.dino.width, n)
+    cur.wait_stream(side)
 
   def encode(self, pixels: torch.Tensor) -> torch.Tensor:
     b = pixels.shape[0]

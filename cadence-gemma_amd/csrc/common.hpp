@@ -38,6 +38,18 @@ CADENCE_DEV float badd(float a, float b) { return rbf(add_rn(a, b)); }
 CADENCE_DEV float bsub(float a, float b) { return rbf(sub_rn(a, b)); }
 
 CADENCE_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+// Hardware transcendentals (v_exp_f32 / v_rcp_f32 / v_sqrt_f32, ~1-2 ulp in
+// fp32) for element chains whose results are rounded to bf16 right after:
+// a flip of the bf16 rounding needs the fp32 error to straddle a bf16
+// midpoint (~1e-5 per op).  Used where an accurate libm chain made the
+// kernel VALU-bound (RG-LRU gate chain).
+CADENCE_DEV float hw_exp(float x) {
+  return __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
+}
+CADENCE_DEV float hw_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + hw_exp(-x));
+}
+CADENCE_DEV float hw_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 CADENCE_DEV float softplusf_(float x) {
   // torch softplus(beta=1, threshold=20)
   return x > 20.0f ? x : log1pf(expf(x));

@@ -27,6 +27,7 @@
 //  EpiVitResid    timm residual: resid += gamma * (x.W + b)   (fp32 stream)
 //  EpiPatch       patch-embed conv as GEMM + pos_embed at a prefix offset
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -42,7 +43,12 @@ constexpr int BK = 64;
 struct RowMap {
   int64_t div, mul, off;  // out_row = (m / div) * mul + (m % div) + off
   CADENCE_DEV int64_t operator()(int64_t m) const {
-    return (m / div) * mul + (m % div) + off;
+    // rows and divisors are < 2^31: 32-bit division (the 64-bit one is a
+    // long inline sequence per call site in the unrolled epilogues)
+    if (mul == 0 && off == 0 && m < div) return m;
+    const uint32_t um = (uint32_t)m, ud = (uint32_t)div;
+    const uint32_t q = um / ud;
+    return (int64_t)q * mul + (int64_t)(um - q * ud) + off;
   }
 };
 
@@ -52,27 +58,38 @@ CADENCE_DEV float softcap(float l, float c) {
   return rbf(rbf(tanhf(t)) * c);
 }
 
-// Epilogue interface: apply / apply2 write one element (direct path);
-// staged epilogues (kStaged) split that into value / value2 (per element,
-// bf16-exact result before any residual) and store8 (8 consecutive output
-// columns of one row, 16-B aligned).
+// Epilogue interface.
+//  * Direct path (legacy tile, stream and split-K engines): apply(m, n, v, g)
+//    / apply2(m, f, v_gate, v_up, g) write one element.
+//  * Staged path (big engine, kStaged): bias_at() + stage() / stage2() take
+//    one accumulator to its first bf16 rounding point (bias added); the
+//    engine parks those in LDS and a ROLLED loop hands 8 consecutive staged
+//    columns of one row to finish8(m, n, v8, g) (paired epilogues:
+//    finish8p(m, f, gate8, up8, g)), which runs the rest of the element
+//    chain and writes 16-B rows.  Keeping activations out of the unrolled
+//    128-element accumulator loop keeps the kernel inside the instruction
+//    cache (an unrolled gate chain made the kernel 160 KB and cost ~25 us of
+//    instruction fetch per tile).
 struct EpiLinear {
   static constexpr bool kPaired = false;
   static constexpr bool kStaged = true;
+  static constexpr bool kTile = false;
   u16* out; int64_t ldo;
   const u16* bias;
   const u16* resid; int64_t ldr;
   int act;                 // 0 none, 1 gelu(erf), 2 soft-cap(cap), 3 gelu(tanh)
   RowMap map;
   float cap;
-  CADENCE_DEV float value(int64_t, int n, float v, int) const {
-    // F.linear adds the bias in fp32 before the single bf16 rounding.
-    if (bias) v = add_rn(v, bf2f(bias[n]));
-    float r = rbf(v);
+  CADENCE_DEV float activate(float r) const {
     if (act == 1) r = rbf(gelu_erf(r));
     if (act == 2) r = softcap(r, cap);
     if (act == 3) r = rbf(gelu_tanh(r));
     return r;
+  }
+  CADENCE_DEV float value(int64_t, int n, float v, int) const {
+    // F.linear adds the bias in fp32 before the single bf16 rounding.
+    if (bias) v = add_rn(v, bf2f(bias[n]));
+    return activate(rbf(v));
   }
   CADENCE_DEV void apply(int64_t m, int n, float v, int g) const {
     float r = value(m, n, v, g);
@@ -80,23 +97,57 @@ struct EpiLinear {
     if (resid) r = badd(r, bf2f(resid[orow * ldr + n]));
     out[orow * ldo + n] = f2bf(r);
   }
-  CADENCE_DEV void store8(int64_t m, int n, uint4 v, int) const {
+  // staged path
+  CADENCE_DEV float bias_at(bool, int n, int) const {
+    return bias ? bf2f(bias[n]) : 0.0f;
+  }
+  CADENCE_DEV float stage(float v, float b) const {
+    if (bias) v = add_rn(v, b);
+    return rbf(v);
+  }
+  template <class Act>
+  CADENCE_DEV void finish8_with(int64_t m, int n, uint4 v, Act&& f) const {
     const int64_t orow = map(m);
+    float a[8];
+    unpack8(v, a);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = f(a[i]);
     if (resid) {
-      float a[8], b[8];
-      unpack8(v, a);
+      float b[8];
       unpack8(ld16(resid + orow * ldr + n), b);
 #pragma unroll
       for (int i = 0; i < 8; ++i) a[i] = badd(a[i], b[i]);
-      v = pack8(a);
     }
-    st16(out + orow * ldo + n, v);
+    st16(out + orow * ldo + n, pack8(a));
+  }
+  CADENCE_DEV void finish8(int64_t m, int n, uint4 v, int) const {
+    finish8_with(m, n, v, [&](float r) { return activate(r); });
+  }
+};
+
+// EpiLinear with the activation fixed at compile time (big engine).
+template <int ACT>
+struct EpiLinearA : EpiLinear {
+  CADENCE_DEV void finish8(int64_t m, int n, uint4 v, int) const {
+    if constexpr (ACT == 0) {
+      if (!resid) {
+        st16(out + map(m) * ldo + n, v);
+        return;
+      }
+    }
+    finish8_with(m, n, v, [&](float r) {
+      if constexpr (ACT == 1) r = rbf(gelu_erf(r));
+      if constexpr (ACT == 2) r = softcap(r, cap);
+      if constexpr (ACT == 3) r = rbf(gelu_tanh(r));
+      return r;
+    });
   }
 };
 
 struct EpiGatedGelu {
   static constexpr bool kPaired = true;
   static constexpr bool kStaged = true;
+  static constexpr bool kTile = false;
   u16* out; int64_t ldo;
   const u16* bias_g; const u16* bias_u;
   CADENCE_DEV float value2(int64_t, int f, float g, float u, int) const {
@@ -108,14 +159,33 @@ struct EpiGatedGelu {
   CADENCE_DEV void apply2(int64_t m, int f, float g, float u, int gg) const {
     out[m * ldo + f] = f2bf(value2(m, f, g, u, gg));
   }
-  CADENCE_DEV void store8(int64_t m, int f, uint4 v, int) const {
-    st16(out + m * ldo + f, v);
+  CADENCE_DEV float bias_at(bool up, int f, int) const {
+    return bf2f((up ? bias_u : bias_g)[f]);
+  }
+  CADENCE_DEV float stage(float v, float b) const { return badd(rbf(v), b); }
+  CADENCE_DEV void finish8p(int64_t m, int f, uint4 g8, uint4 u8, int) const {
+    float gv[8], uv[8];
+    unpack8(g8, gv);
+    unpack8(u8, uv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gv[i] = bmul(rbf(gelu_tanh(gv[i])), uv[i]);
+    st16(out + m * ldo + f, pack8(gv));
   }
 };
 
+// Tile epilogues (kTile): the big engine hands the whole wave tile
+// (acc[MR][4], rows mbase + 16 i + 4 (lane >> 4) + r, columns
+// nbase + 16 j + (lane & 15)) to `tile`, which issues its global loads in
+// batches ahead of the stores (element-wise load -> store through possibly
+// aliasing pointers serialises one load latency per element).
+template <int MR>
+using AccTile = f32x4[MR][4];
+
+// RG-LRU gate chain (layers.py:345-365) on the block-diagonal gate GEMM.
 struct EpiRglruGates {
   static constexpr bool kPaired = true;
-  static constexpr bool kStaged = false;
+  static constexpr bool kStaged = true;
+  static constexpr bool kTile = false;
   const u16* x; int64_t ldx;         // conv1d output (RG-LRU input)
   const u16* bias_x; const u16* bias_a;
   const u16* softplus_a;             // bf16(softplus(a_param)), [E]
@@ -128,18 +198,24 @@ struct EpiRglruGates {
   float* h; int64_t ldh;
   const u16* gate; int64_t ldg;
   u16* y_out; int64_t ldy;
+  // gx_pre / ga_pre are the bf16 BDL outputs (einsum rounded, + b rounded).
+  CADENCE_DEV void chain(float gx_pre, float ga_pre, float xv, float sp,
+                         bool reset, float& av, float& nx) const {
+    const float gx = rbf(hw_sigmoid(gx_pre));
+    const float ga = rbf(hw_sigmoid(ga_pre));
+    const float log_a = bmul(rbf(-8.0f * ga), sp);
+    const float a = rbf(hw_exp(log_a));
+    const float a_sq = rbf(hw_exp(rbf(2.0f * log_a)));
+    const float gated = bmul(xv, gx);
+    const float mult = reset ? 1.0f : rbf(hw_sqrt(rbf(1.0f - a_sq)));
+    av = reset ? 0.0f : a;
+    nx = bmul(gated, mult);
+  }
   CADENCE_DEV void apply2(int64_t m, int j, float accx, float acca, int g) const {
     const int e = g * bw + j;
-    const float gx = rbf(sigmoidf_(badd(rbf(accx), bf2f(bias_x[e]))));
-    const float ga = rbf(sigmoidf_(badd(rbf(acca), bf2f(bias_a[e]))));
-    const float log_a = bmul(rbf(-8.0f * ga), bf2f(softplus_a[e]));
-    const float a = rbf(expf(log_a));
-    const float a_sq = rbf(expf(rbf(2.0f * log_a)));
-    const float gated = bmul(bf2f(x[m * ldx + e]), gx);
-    const bool reset = segpos[m] == 0;
-    const float mult = reset ? 1.0f : rbf(sqrtf(rbf(1.0f - a_sq)));
-    const float av = reset ? 0.0f : a;
-    const float nx = bmul(gated, mult);
+    float av, nx;
+    chain(badd(rbf(accx), bf2f(bias_x[e])), badd(rbf(acca), bf2f(bias_a[e])),
+          bf2f(x[m * ldx + e]), bf2f(softplus_a[e]), segpos[m] == 0, av, nx);
     if (h) {
       float* hp = h + m * ldh + e;
       const float hn = add_rn(mul_rn(av, *hp), nx);
@@ -152,11 +228,44 @@ struct EpiRglruGates {
     a_out[m * ldo + e] = f2bf(av);
     nx_out[m * ldo + e] = f2bf(nx);
   }
+  CADENCE_DEV float bias_at(bool up, int j, int g) const {
+    return bf2f((up ? bias_a : bias_x)[g * bw + j]);
+  }
+  CADENCE_DEV float stage(float v, float b) const { return badd(rbf(v), b); }
+  CADENCE_DEV void finish8p(int64_t m, int j, uint4 gx8, uint4 ga8, int g) const {
+    const int e = g * bw + j;
+    float gx[8], ga[8], xv[8], sp[8];
+    unpack8(gx8, gx);
+    unpack8(ga8, ga);
+    unpack8(ld16(x + m * ldx + e), xv);
+    unpack8(ld16(softplus_a + e), sp);
+    const bool reset = segpos[m] == 0;
+    float av[8], nx[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) chain(gx[i], ga[i], xv[i], sp[i], reset, av[i], nx[i]);
+    if (h) {
+      float* hp = h + m * ldh + e;
+      float y[8], gv[8];
+      if (gate) unpack8(ld16(gate + m * ldg + e), gv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float hn = add_rn(mul_rn(av[i], hp[i]), nx[i]);
+        hp[i] = hn;
+        y[i] = rbf(hn);
+        if (gate) y[i] = bmul(y[i], gv[i]);
+      }
+      st16(y_out + m * ldy + e, pack8(y));
+      return;
+    }
+    st16(a_out + m * ldo + e, pack8(av));
+    st16(nx_out + m * ldo + e, pack8(nx));
+  }
 };
 
 struct EpiVitResid {
   static constexpr bool kPaired = false;
   static constexpr bool kStaged = false;
+  static constexpr bool kTile = true;
   float* resid; int64_t ldr;
   const u16* bias; const u16* gamma;
   CADENCE_DEV void apply(int64_t m, int n, float v, int) const {
@@ -164,11 +273,53 @@ struct EpiVitResid {
     if (gamma) v *= bf2f(gamma[n]);
     resid[m * ldr + n] += v;
   }
+  // resid += gamma * (acc + bias): the residual rows are read two row
+  // groups (32 values per lane) at a time ahead of their stores.
+  template <int MR>
+  CADENCE_DEV void tile(const AccTile<MR>& acc, int64_t mbase, int nbase,
+                        int lane, int M, int N, int) const {
+    const int rsub = (lane >> 4) * 4, csub = lane & 15;
+    int col[4];
+    float bv[4], gv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      col[j] = min(nbase + j * 16 + csub, N - 1);
+      bv[j] = bf2f(bias[col[j]]);
+      gv[j] = gamma ? bf2f(gamma[col[j]]) : 1.0f;
+    }
+#pragma unroll
+    for (int i0 = 0; i0 < MR; i0 += 2) {
+      float rv[2][4][4];
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = min<int64_t>(mbase + (i0 + ii) * 16 + rsub + r, M - 1);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rv[ii][j][r] = resid[row * ldr + col[j]];
+        }
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = mbase + (i0 + ii) * 16 + rsub + r;
+          if (row >= M) continue;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (nbase + j * 16 + csub >= N) continue;
+            float v = acc[i0 + ii][j][r] + bv[j];
+            if (gamma) v *= gv[j];
+            resid[row * ldr + col[j]] = rv[ii][j][r] + v;
+          }
+        }
+    }
+  }
 };
 
 struct EpiPatch {
   static constexpr bool kPaired = false;
   static constexpr bool kStaged = false;
+  static constexpr bool kTile = true;
   float* resid;                      // [B, ntok, N] fp32
   const u16* bias; const u16* pos;   // pos [P, N]
   int64_t P, ntok, prefix, N;
@@ -177,6 +328,48 @@ struct EpiPatch {
     v += bf2f(bias[n]);
     v += bf2f(pos[p * N + n]);
     resid[(b * ntok + prefix + p) * N + n] = v;
+  }
+  template <int MR>
+  CADENCE_DEV void tile(const AccTile<MR>& acc, int64_t mbase, int nbase,
+                        int lane, int M, int Ncols, int) const {
+    const int rsub = (lane >> 4) * 4, csub = lane & 15;
+    int col[4];
+    float bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      col[j] = min(nbase + j * 16 + csub, Ncols - 1);
+      bv[j] = bf2f(bias[col[j]]);
+    }
+#pragma unroll
+    for (int i0 = 0; i0 < MR; i0 += 2) {
+      float pv[2][4][4];
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = min<int64_t>(mbase + (i0 + ii) * 16 + rsub + r, M - 1);
+          const uint32_t pr = (uint32_t)row % (uint32_t)P;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pv[ii][j][r] = bf2f(pos[(int64_t)pr * N + col[j]]);
+        }
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = mbase + (i0 + ii) * 16 + rsub + r;
+          if (row >= M) continue;
+          const uint32_t b = (uint32_t)row / (uint32_t)P;
+          const uint32_t p = (uint32_t)row - b * (uint32_t)P;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (nbase + j * 16 + csub >= Ncols) continue;
+            float v = acc[i0 + ii][j][r];
+            v += bv[j];
+            v += pv[ii][j][r];
+            resid[((int64_t)b * ntok + prefix + p) * N + col[j]] = v;
+          }
+        }
+    }
   }
 };
 
@@ -423,47 +616,56 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
   const int mbase = m0 + wm * 128, nbase = n0 + wn * 64;
   const int rsub = (lane >> 4) * 4, csub = lane & 15;
   if constexpr (Epi::kStaged) {
-    // Stage the wave's bf16 results in its own 16 KiB of the (now idle)
-    // operand LDS, [128 rows][OC cols] with a 16-B chunk XOR swizzle, then
-    // write whole 16-B row segments (one store instruction per 8 rows).
+    // Stage the wave's first-rounding-point bf16 values in its own 16 KiB of
+    // the (now idle) operand LDS, [128 rows][64 cols] with a 16-B chunk XOR
+    // swizzle (paired: cols 0..31 gate half, 32..63 up half of the same 32
+    // logical columns), then a rolled loop finishes 8 columns of one row per
+    // lane and writes 16-B row segments.
     constexpr int OC = Epi::kPaired ? 32 : 64;     // output columns per wave
-    constexpr int CPRW = OC / 8;                   // 16-B chunks per row
+    constexpr int CPRW = OC / 8;                   // 16-B output chunks per row
     __syncthreads();   // every wave is done reading the operand buffers
     if (nbase >= N) return;   // wave-uniform: this wave's columns are padding
     u16* st = reinterpret_cast<u16*>(smem) + wave * (128 * 64);
     auto sidx = [&](int r, int c) {
-      return r * OC + (((c >> 3) ^ (r & (CPRW - 1))) << 3) + (c & 7);
+      return r * 64 + (((c >> 3) ^ (r & 7)) << 3) + (c & 7);
     };
+    float bcol[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      if constexpr (Epi::kPaired)
+        bcol[j] = epi.bias_at(j >= 2, nbase / 2 + (j & 1) * 16 + csub, g);
+      else
+        bcol[j] = epi.bias_at(false, min(nbase + j * 16 + csub, N - 1), g);
+    }
 #pragma unroll
     for (int i = 0; i < MR; ++i)
 #pragma unroll
-      for (int j = 0; j < (Epi::kPaired ? 2 : NR); ++j)
+      for (int j = 0; j < NR; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int lr = i * 16 + rsub + r;
-          const int lc = j * 16 + csub;
-          float v;
-          if constexpr (Epi::kPaired)
-            v = epi.value2(mbase + lr, nbase / 2 + lc, acc[i][j][r],
-                           acc[i][j + 2][r], g);
-          else
-            v = epi.value(mbase + lr, min(nbase + lc, N - 1), acc[i][j][r], g);
-          st[sidx(lr, lc)] = f2bf(v);
-        }
+        for (int r = 0; r < 4; ++r)
+          st[sidx(i * 16 + rsub + r, j * 16 + csub)] =
+              f2bf(epi.stage(acc[i][j][r], bcol[j]));
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    constexpr int RPI = 64 / CPRW;                 // rows per store instruction
+    constexpr int RPI = 64 / CPRW;                 // rows per iteration
     const int obase = Epi::kPaired ? nbase / 2 : nbase;
-#pragma unroll
+    const int ch = lane % CPRW;
+#pragma unroll 2
     for (int it = 0; it < 128 / RPI; ++it) {
       const int lr = it * RPI + lane / CPRW;
-      const int ch = lane % CPRW;
       const int row = mbase + lr;
       const int col = obase + ch * 8;
-      const uint4 v = *reinterpret_cast<const uint4*>(
-          &st[lr * OC + ((ch ^ (lr & (CPRW - 1))) << 3)]);
-      if (row < M && (Epi::kPaired || col < N)) epi.store8(row, col, v, g);
+      const uint4 v = *reinterpret_cast<const uint4*>(&st[lr * 64 + ((ch ^ (lr & 7)) << 3)]);
+      if constexpr (Epi::kPaired) {
+        const uint4 u = *reinterpret_cast<const uint4*>(
+            &st[lr * 64 + (((ch + 4) ^ (lr & 7)) << 3)]);
+        if (row < M) epi.finish8p(row, col, v, u, g);
+      } else {
+        if (row < M && col < N) epi.finish8(row, col, v, g);
+      }
     }
+  } else if constexpr (Epi::kTile) {
+    epi.template tile<MR>(acc, mbase, nbase, lane, M, N, g);
   } else if constexpr (Epi::kPaired) {
 #pragma unroll
     for (int i = 0; i < MR; ++i)
@@ -933,8 +1135,23 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
     }
     const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
     dim3 grid((unsigned)tiles, (unsigned)groups);
-    hipLaunchKernelGGL((gemm_big_kernel<Epi>), grid, dim3(512), 0, st, A, lda, W,
-                       ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
+    if constexpr (std::is_same_v<Epi, EpiLinear>) {
+#define CADENCE_BIG_ACT(ACT_)                                                          \
+  hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>>), grid, dim3(512), 0, st, A, \
+                     lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff,            \
+                     EpiLinearA<ACT_>{epi})
+      switch (epi.act) {
+        case 0: CADENCE_BIG_ACT(0); break;
+        case 1: CADENCE_BIG_ACT(1); break;
+        case 2: CADENCE_BIG_ACT(2); break;
+        case 3: CADENCE_BIG_ACT(3); break;
+        default: return (int)hipErrorInvalidValue;
+      }
+#undef CADENCE_BIG_ACT
+    } else {
+      hipLaunchKernelGGL((gemm_big_kernel<Epi>), grid, dim3(512), 0, st, A, lda, W,
+                         ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
+    }
     return (int)hipGetLastError();
   }
   if (N % 64 || K % 32) return (int)hipErrorInvalidValue;
