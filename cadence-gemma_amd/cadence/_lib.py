@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -61,7 +61,7 @@ _SIGS: dict[str, list] = {
     "cadence_local_attention": [P, P, P, P, P, P, I64, I64, I64, I64, I64, P],
     "cadence_kv_cache_fill": [P, P, P, P, P, P, I64, I64, I64, I64, P],
     "cadence_local_attention_decode": [P, P, P, P, P, P, P, I64, I64, I64, I64,
-                                       P, I64, P, P],
+                                       I64, P, I64, P, P],
     "cadence_local_attention_decode_workspace_bytes": [I64, I64],
     "cadence_im2col_normalize": [P, P, I64, I64, I64, I64, P, P, P],
     "cadence_vit_prefix": [P, P, I64, I64, I64, I64, P],

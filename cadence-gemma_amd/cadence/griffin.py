@@ -121,7 +121,8 @@ class Griffin(nn.Module):
           x, pos, b, length, None if cache is None else cache[name],
           return_cache, inplace_state, xn, nxt)
     if final_norm and xn is None:
-      xn = ops.rmsnorm(x, self.final_norm.scale, self.final_norm.eps)
+      xn = ops.rmsnorm(x, self.final_norm.scale, self.final_norm.eps,
+                       packed=True)
     return x, xn, new_cache
 
   # ------------------------------------------------------------------ API

@@ -187,11 +187,13 @@ class RGLRU(nn.Module):
     return ops.rglru_gates(x2d, w, bx, ba, sp, pos_flat)
 
   def step_(self, x2d: torch.Tensor, pos_flat: torch.Tensor, h: torch.Tensor,
-            gate: torch.Tensor | None = None) -> torch.Tensor:
+            gate: torch.Tensor | None = None, packed_out: bool = False):
     """One token per row (T = 1): gates + scan step fused, `h` updated in
-    place; returns bf16(h) [* gate]."""
+    place; returns bf16(h) [* gate] (PackedRows when `packed_out` and the
+    rows qualify: the decode path's linear_out consumes it)."""
     w, bx, ba, sp = self.packed()
-    return ops.rglru_step_(x2d, w, bx, ba, sp, pos_flat, h, gate)
+    return ops.rglru_step_(x2d, w, bx, ba, sp, pos_flat, h, gate,
+                           None if packed_out else False)
 
   def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,
               cache: torch.Tensor | None = None, return_cache: bool = True):

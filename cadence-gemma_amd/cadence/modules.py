@@ -117,8 +117,8 @@ class LocalAttentionBlock(nn.Module):
       if t != 1:
         # reference modules.py:206-225 only supports 1 or >= window tokens
         raise NotImplementedError()
-      enc = ops.ops.local_attention_decode_(q, k, v, cache.keys, cache.values,
-                                            cache.num_tokens, h)
+      enc = ops.local_attention_decode_(q, k, v, cache.keys, cache.values,
+                                        cache.num_tokens, h)
       new_cache = cache if return_cache else None
     out, hn = _out_proj(enc, self.proj_final, resid2d, norm)
     return out, hn, new_cache
@@ -203,7 +203,7 @@ class RecurrentBlock(nn.Module):
       conv_out = ops.ops.conv1d_step_(x_br, self.conv_1d.w, self.conv_1d.b,
                                       cache.conv1d_state)
       gated = self.rg_lru.step_(conv_out, pos.view(-1), cache.rg_lru_state,
-                                y_br)
+                                y_br, packed_out=True)
       out, hn = _out_proj(gated, self.linear_out, resid2d, norm)
       return out, hn, cache
     conv_out, conv_state = self.conv_1d.apply2d(
@@ -331,7 +331,7 @@ class ResidualBlock(nn.Module):
     None, cache)."""
     if xn is None:
       xn = ops.rmsnorm(x2d, self.temporal_pre_norm.scale,
-                       self.temporal_pre_norm.eps)
+                       self.temporal_pre_norm.eps, packed=True)
     if self.temporal_block_type == common.TemporalBlockType.RECURRENT:
       resid, hn, new_cache = self.recurrent_block.fused(
           xn, pos, b, t, cache, return_cache, x2d, inplace_state,

@@ -13,6 +13,9 @@ what the modules call; they route through `torch.ops.cadence`.
 
 from __future__ import annotations
 
+import os
+from typing import NamedTuple
+
 import torch
 
 from . import _lib
@@ -128,6 +131,68 @@ def _ws(M: int, N: int, K: int, groups: int, like: torch.Tensor):
   return torch.empty(n, dtype=torch.uint8, device=like.device), n
 
 
+# ------------------------------------------------------ packed decode rows
+
+DECODE_PACKED = os.environ.get("CADENCE_DECODE_PACKED", "1") != "0"
+
+
+class PackedRows(NamedTuple):
+  """M <= 32 activation rows in the decode fragment layout
+  (include/cadence_kernels.h "Decode activation layout"): what the decode
+  producers (RMSNorm, gated GELU, RG-LRU step, decode attention) emit and
+  the decode GEMVs consume, so each wave's activation load is 1 KiB of
+  contiguous bytes.  `data` is a flat bf16 tensor of k * 16 * ceil(m/16)."""
+  data: torch.Tensor
+  m: int
+  k: int
+
+  @property
+  def shape(self):
+    return (self.m, self.k)
+
+  @property
+  def device(self):
+    return self.data.device
+
+  @property
+  def dtype(self):
+    return self.data.dtype
+
+  def unpack(self) -> torch.Tensor:
+    """Row-major [m, k] copy (tests / debugging)."""
+    mt = -(-self.m // 16)
+    x = self.data.view(self.k // 32, mt, 4, 16, 8).permute(1, 3, 0, 2, 4)
+    return x.reshape(mt * 16, self.k)[: self.m]
+
+
+def want_packed(m: int, k: int) -> bool:
+  return DECODE_PACKED and 0 < m <= 32 and k % 32 == 0
+
+
+def packed_empty(m: int, k: int, device) -> torch.Tensor:
+  return torch.empty(k * 16 * (-(-m // 16)), dtype=_BF16, device=device)
+
+
+def pack_rows(x: torch.Tensor) -> PackedRows:
+  """Row-major [m, k] -> PackedRows (torch ops; tests and one-off use)."""
+  m, k = x.shape
+  mt = -(-m // 16)
+  xp = torch.zeros(mt * 16, k, dtype=x.dtype, device=x.device)
+  xp[:m] = x
+  data = xp.view(mt, 16, k // 32, 4, 8).permute(2, 0, 3, 1, 4).contiguous().view(-1)
+  return PackedRows(data, m, k)
+
+
+def _arows(a, name: str):
+  """(tensor to pass, lda, M, K) of a GEMM A operand: a row-major view or
+  PackedRows (lda 0)."""
+  if isinstance(a, PackedRows):
+    _need(a.data.dtype == _BF16 and a.data.is_contiguous(), f"{name}: packed rows")
+    return a.data, 0, a.m, a.k
+  lda = _mat(a, name)
+  return a, lda, a.shape[0], a.shape[1]
+
+
 # ------------------------------------------------------------------- GEMMs
 
 # ------------------------------------------------- decode weight layout
@@ -169,12 +234,18 @@ def _wld(w, packed: bool, name: str) -> int:
 
 @_reg("gemm_linear_(Tensor a, Tensor w, Tensor? bias, Tensor? resid, "
       "Tensor(a!) out, int act, int row_div, int row_mul, int row_off, "
-      "bool w_packed=False) -> ()")
+      "bool w_packed=False, int a_rows=-1) -> ()")
 def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off,
-                 w_packed=False):
-  lda, ldw, ldo = _mat(a, "a"), _wld(w, w_packed, "w"), _mat(out, "out")
-  M, K = a.shape
-  N = w.shape[0]
+                 w_packed=False, a_rows=-1):
+  """a_rows >= 0: `a` is PackedRows data of a_rows rows (lda 0)."""
+  ldw, ldo = _wld(w, w_packed, "w"), _mat(out, "out")
+  N, K = w.shape[0], w.shape[1]
+  if a_rows >= 0:
+    lda, M = 0, a_rows
+    _need(a.numel() == K * 16 * (-(-M // 16)), "a: packed rows size")
+  else:
+    lda = _mat(a, "a")
+    M, K = a.shape
   _need(w.shape[1] == K, f"K mismatch {K} vs {w.shape[1]}")
   ldr = 0
   if resid is not None:
@@ -190,15 +261,23 @@ def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off,
 
 
 @_reg("gemm_linear_rmsnorm(Tensor a, Tensor w, Tensor? bias, Tensor? resid, "
-      "Tensor scale, float eps, bool w_packed=False) -> (Tensor, Tensor)")
-def _gemm_linear_rmsnorm(a, w, bias, resid, scale, eps, w_packed=False):
-  """(out, rmsnorm(out)): out = a . w^T + bias (+ resid)."""
-  lda, ldw = _mat(a, "a"), _wld(w, w_packed, "w")
-  M, K = a.shape
-  N = w.shape[0]
+      "Tensor scale, float eps, bool w_packed=False, int a_rows=-1, "
+      "bool norm_packed=False) -> (Tensor, Tensor)")
+def _gemm_linear_rmsnorm(a, w, bias, resid, scale, eps, w_packed=False,
+                         a_rows=-1, norm_packed=False):
+  """(out, rmsnorm(out)): out = a . w^T + bias (+ resid).  a_rows >= 0: `a`
+  is PackedRows data; norm_packed: rmsnorm(out) as PackedRows data."""
+  ldw = _wld(w, w_packed, "w")
+  N, K = w.shape[0], w.shape[1]
+  if a_rows >= 0:
+    lda, M = 0, a_rows
+  else:
+    lda = _mat(a, "a")
+    M, K = a.shape
   ldr = _mat(resid, "resid") if resid is not None else 0
   out = torch.empty(M, N, dtype=_BF16, device=a.device)
-  nout = torch.empty(M, N, dtype=_BF16, device=a.device)
+  nout = (packed_empty(M, N, a.device) if norm_packed else
+          torch.empty(M, N, dtype=_BF16, device=a.device))
   lib = _lib.load()
   nws = max(lib.cadence_gemm_rmsnorm_workspace_bytes(M, N, K),
             lib.cadence_gemm_workspace_bytes(M, N, K, 1))
@@ -206,25 +285,34 @@ def _gemm_linear_rmsnorm(a, w, bias, resid, scale, eps, w_packed=False):
   ev = TIMER.start(a) if _tile(M) else None
   _lib.check(lib.cadence_gemm_linear_rmsnorm(
       _p(a), lda, _p(w), ldw, _p(bias), _p(resid), ldr, _p(out), N, M, N, K,
-      _p(scale), float(eps), _p(nout), N, _p(ws), nws, _s(a)),
+      _p(scale), float(eps), _p(nout), 0 if norm_packed else N, _p(ws), nws,
+      _s(a)),
       "gemm_linear_rmsnorm")
   TIMER.stop(ev, "gemm_tile_kernel<EpiLinear>", 2.0 * M * N * K, a)
   return out, nout
 
 
 @_reg("gated_gelu(Tensor a, Tensor w_packed, Tensor bias_gate, "
-      "Tensor bias_up, bool decode_layout=False) -> Tensor")
-def _gated_gelu(a, w_packed, bias_gate, bias_up, decode_layout=False):
-  lda = _mat(a, "a")
-  M, K = a.shape
-  F = w_packed.shape[0] // 2
-  _need(w_packed.shape[1] == K and w_packed.is_contiguous(), "w_packed")
-  out = torch.empty(M, F, dtype=_BF16, device=a.device)
+      "Tensor bias_up, bool decode_layout=False, int a_rows=-1, "
+      "bool out_packed=False) -> Tensor")
+def _gated_gelu(a, w_packed, bias_gate, bias_up, decode_layout=False, a_rows=-1,
+                out_packed=False):
+  F, K = w_packed.shape[0] // 2, w_packed.shape[1]
+  if a_rows >= 0:
+    lda, M = 0, a_rows
+  else:
+    lda = _mat(a, "a")
+    M = a.shape[0]
+    _need(a.shape[1] == K, "a / w_packed K mismatch")
+  _need(w_packed.is_contiguous(), "w_packed")
+  out = (packed_empty(M, F, a.device) if out_packed else
+         torch.empty(M, F, dtype=_BF16, device=a.device))
   ws, nws = _ws(M, 2 * F, K, 1, a)
   ev = TIMER.start(a) if _tile(M) else None
   _lib.check(_lib.load().cadence_gemm_gated_gelu(
       _p(a), lda, _p(w_packed), 0 if decode_layout else K, _p(bias_gate),
-      _p(bias_up), _p(out), F, M, F, K, _p(ws), nws, _s(a)), "gated_gelu")
+      _p(bias_up), _p(out), 0 if out_packed else F, M, F, K, _p(ws), nws, _s(a)),
+      "gated_gelu")
   TIMER.stop(ev, "gemm_tile_kernel<EpiGatedGelu>", 4.0 * M * F * K, a)
   return out
 
@@ -254,9 +342,9 @@ def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos,
 
 @_reg("rglru_step_(Tensor x, Tensor w_packed, Tensor bias_x, Tensor bias_a, "
       "Tensor softplus_a, Tensor segment_pos, Tensor(a!) h, Tensor? gate, "
-      "bool decode_layout=False) -> Tensor")
+      "bool decode_layout=False, bool out_packed=False) -> Tensor")
 def _rglru_step(x, w_packed, bias_x, bias_a, softplus_a, segment_pos, h, gate,
-                decode_layout=False):
+                decode_layout=False, out_packed=False):
   """Gate GEMM + chain + the T == 1 scan step; `h` [M, E] fp32 in place."""
   ldx = _mat(x, "x")
   M, E = x.shape
@@ -266,12 +354,14 @@ def _rglru_step(x, w_packed, bias_x, bias_a, softplus_a, segment_pos, h, gate,
   _need(h.dtype == _F32 and h.is_contiguous() and tuple(h.shape) == (M, E),
         "h: [M, E] fp32 contiguous")
   ldg = _mat(gate, "gate") if gate is not None else 0
-  y = torch.empty(M, E, dtype=_BF16, device=x.device)
+  y = (packed_empty(M, E, x.device) if out_packed else
+       torch.empty(M, E, dtype=_BF16, device=x.device))
   ws, nws = _ws(M, 2 * bw, bw, H, x)
   _lib.check(_lib.load().cadence_rglru_step(
       _p(x), ldx, _p(w_packed), 0 if decode_layout else bw, _p(bias_x),
       _p(bias_a), _p(softplus_a), _p(segment_pos.contiguous()), _p(h),
-      _p(gate), ldg, _p(y), E, M, H, bw, _p(ws), nws, _s(x)), "rglru_step")
+      _p(gate), ldg, _p(y), 0 if out_packed else E, M, H, bw, _p(ws), nws,
+      _s(x)), "rglru_step")
   return y
 
 
@@ -303,10 +393,16 @@ def _patch_embed(patches, w, bias, pos, resid, B, P, ntok, prefix):
 
 
 @_reg("logits_argmax(Tensor x, Tensor embedding, float soft_cap, "
-      "bool return_logits, bool decode_layout=False) -> (Tensor, Tensor)")
-def _logits_argmax(x, embedding, soft_cap, return_logits, decode_layout=False):
-  ldx = _mat(x, "x")
-  M, D = x.shape
+      "bool return_logits, bool decode_layout=False, int a_rows=-1) "
+      "-> (Tensor, Tensor)")
+def _logits_argmax(x, embedding, soft_cap, return_logits, decode_layout=False,
+                   a_rows=-1):
+  D = embedding.shape[1]
+  if a_rows >= 0:
+    ldx, M = 0, a_rows
+  else:
+    ldx = _mat(x, "x")
+    M, D = x.shape
   V = embedding.shape[0]
   L = _lib.load()
   nscr = L.cadence_logits_scratch_bytes(M, V, D)
@@ -323,10 +419,14 @@ def _logits_argmax(x, embedding, soft_cap, return_logits, decode_layout=False):
 
 
 @_reg("gemm_logits(Tensor x, Tensor embedding, float soft_cap, "
-      "bool decode_layout=False) -> Tensor")
-def _gemm_logits(x, embedding, soft_cap, decode_layout=False):
-  ldx = _mat(x, "x")
-  M, D = x.shape
+      "bool decode_layout=False, int a_rows=-1) -> Tensor")
+def _gemm_logits(x, embedding, soft_cap, decode_layout=False, a_rows=-1):
+  D = embedding.shape[1]
+  if a_rows >= 0:
+    ldx, M = 0, a_rows
+  else:
+    ldx = _mat(x, "x")
+    M, D = x.shape
   V = embedding.shape[0]
   out = torch.empty(M, V, dtype=_BF16, device=x.device)
   ws, nws = _ws(M, V, D, 1, x)
@@ -338,13 +438,15 @@ def _gemm_logits(x, embedding, soft_cap, decode_layout=False):
 
 # ------------------------------------------------------ norms / embedding
 
-@_reg("rmsnorm(Tensor x, Tensor scale, float eps) -> Tensor")
-def _rmsnorm(x, scale, eps):
+@_reg("rmsnorm(Tensor x, Tensor scale, float eps, bool out_packed=False) "
+      "-> Tensor")
+def _rmsnorm(x, scale, eps, out_packed=False):
   ldx = _mat(x, "x")
-  out = torch.empty(x.shape, dtype=_BF16, device=x.device)
+  out = (packed_empty(x.shape[0], x.shape[1], x.device) if out_packed else
+         torch.empty(x.shape, dtype=_BF16, device=x.device))
   _lib.check(_lib.load().cadence_rmsnorm(
-      _p(x), ldx, _p(scale), _p(out), x.shape[1], x.shape[0], x.shape[1],
-      float(eps), _s(x)), "rmsnorm")
+      _p(x), ldx, _p(scale), _p(out), 0 if out_packed else x.shape[1],
+      x.shape[0], x.shape[1], float(eps), _s(x)), "rmsnorm")
   return out
 
 
@@ -517,22 +619,25 @@ def _kv_cache_fill(k, v, segment_pos, window):
 
 
 @_reg("local_attention_decode_(Tensor q, Tensor k_new, Tensor v_new, "
-      "Tensor(a!) cache_k, Tensor(b!) cache_v, Tensor(c!) num_tokens, int H) "
-      "-> Tensor")
-def _local_attention_decode(q, k_new, v_new, cache_k, cache_v, num_tokens, H):
+      "Tensor(a!) cache_k, Tensor(b!) cache_v, Tensor(c!) num_tokens, int H, "
+      "bool out_packed=False) -> Tensor")
+def _local_attention_decode(q, k_new, v_new, cache_k, cache_v, num_tokens, H,
+                            out_packed=False):
   B = q.shape[0]
   hd = k_new.shape[-1]
   W = cache_k.shape[1]
   _need(cache_k.is_contiguous() and cache_v.is_contiguous(), "cache layout")
   _need(num_tokens.dtype == _I32, "num_tokens int32")
-  out = torch.empty(B, H * hd, dtype=_BF16, device=q.device)
+  out = (packed_empty(B, H * hd, q.device) if out_packed else
+         torch.empty(B, H * hd, dtype=_BF16, device=q.device))
   lib = _lib.load()
   nws = lib.cadence_local_attention_decode_workspace_bytes(B, hd)
   ws = torch.empty(nws, dtype=torch.uint8, device=q.device)
   sems = _counters(q.device, B)
   _lib.check(lib.cadence_local_attention_decode(
       _p(q.contiguous()), _p(k_new.contiguous()), _p(v_new.contiguous()),
-      _p(cache_k), _p(cache_v), _p(num_tokens), _p(out), B, H, hd, W,
+      _p(cache_k), _p(cache_v), _p(num_tokens), _p(out),
+      0 if out_packed else H * hd, B, H, hd, W,
       _p(ws) if sems is not None else None, nws, _p(sems), _s(q)),
       "local_attention_decode")
   return out
@@ -612,37 +717,56 @@ def _decode_advance(next_token, tokens_out, step, positions):
 ops = torch.ops.cadence
 
 
+def _a(x):
+  """(tensor, a_rows) of an A operand: PackedRows -> (data, m), else (x, -1)."""
+  if isinstance(x, PackedRows):
+    return x.data, x.m
+  return x, -1
+
+
 def linear(x2d, w, bias=None, act=0, resid=None, out=None,
            row_map=None):
-  """out = act(x2d . w^T + bias) (+ resid); w [N, K] (nn.Linear layout)."""
+  """out = act(x2d . w^T + bias) (+ resid); w [N, K] (nn.Linear layout).
+  `x2d` may be PackedRows (decode rows)."""
   M = x2d.shape[0]
   N = w.shape[0]
   if out is None:
     out = torch.empty(M, N, dtype=_BF16, device=x2d.device)
   div, mul, off = row_map if row_map is not None else (max(M, 1), 0, 0)
+  a, ar = _a(x2d)
   wd = decode_weight(w) if M <= 32 else None
   if wd is not None:
-    ops.gemm_linear_(x2d, wd, bias, resid, out, act, div, mul, off, True)
+    ops.gemm_linear_(a, wd, bias, resid, out, act, div, mul, off, True, ar)
   else:
-    ops.gemm_linear_(x2d, w, bias, resid, out, act, div, mul, off)
+    ops.gemm_linear_(a, w, bias, resid, out, act, div, mul, off, False, ar)
   return out
 
 
-def linear_rmsnorm(x2d, w, bias, resid, norm):
-  """(x2d . w^T + bias + resid, norm(that)) for a layers.RMSNorm `norm`."""
-  wd = decode_weight(w) if x2d.shape[0] <= 32 else None
-  if wd is not None:
-    return ops.gemm_linear_rmsnorm(x2d, wd, bias, resid, norm.scale, norm.eps,
-                                   True)
-  return ops.gemm_linear_rmsnorm(x2d, w, bias, resid, norm.scale, norm.eps)
+def linear_rmsnorm(x2d, w, bias, resid, norm, packed_out=None):
+  """(x2d . w^T + bias + resid, norm(that)) for a layers.RMSNorm `norm`; the
+  norm output is PackedRows for decode rows (it only feeds GEMMs)."""
+  M, N = x2d.shape[0], w.shape[0]
+  if packed_out is None:
+    packed_out = want_packed(M, N)
+  a, ar = _a(x2d)
+  wd = decode_weight(w) if M <= 32 else None
+  out, nout = ops.gemm_linear_rmsnorm(a, wd if wd is not None else w, bias, resid,
+                                      norm.scale, norm.eps, wd is not None, ar,
+                                      packed_out)
+  return out, (PackedRows(nout, M, N) if packed_out else nout)
 
 
-def gated_gelu(x2d, w_packed, bias_gate, bias_up):
-  """MLP up + gate (packed [2F, K] weight); decode rows use its packed copy."""
-  wd = decode_weight(w_packed) if x2d.shape[0] <= 32 else None
-  if wd is not None:
-    return ops.gated_gelu(x2d, wd, bias_gate, bias_up, True)
-  return ops.gated_gelu(x2d, w_packed, bias_gate, bias_up)
+def gated_gelu(x2d, w_packed, bias_gate, bias_up, packed_out=None):
+  """MLP up + gate (packed [2F, K] weight); decode rows use its packed copy
+  and emit PackedRows (the output only feeds ffw_down)."""
+  M, F = x2d.shape[0], w_packed.shape[0] // 2
+  if packed_out is None:
+    packed_out = want_packed(M, F)
+  a, ar = _a(x2d)
+  wd = decode_weight(w_packed) if M <= 32 else None
+  out = ops.gated_gelu(a, wd if wd is not None else w_packed, bias_gate, bias_up,
+                       wd is not None, ar, packed_out)
+  return PackedRows(out, M, F) if packed_out else out
 
 
 def rglru_gates(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat):
@@ -652,28 +776,49 @@ def rglru_gates(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat):
   return ops.rglru_gates(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat)
 
 
-def rglru_step_(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat, h, gate):
-  wd = decode_weight(w_packed) if x2d.shape[0] <= 32 else None
-  if wd is not None:
-    return ops.rglru_step_(x2d, wd, bias_x, bias_a, softplus_a, pos_flat, h,
-                           gate, True)
-  return ops.rglru_step_(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat, h,
-                         gate)
+def rglru_step_(x2d, w_packed, bias_x, bias_a, softplus_a, pos_flat, h, gate,
+                packed_out=None):
+  """Gate GEMM + chain + scan step; y is PackedRows for decode rows (it only
+  feeds linear_out)."""
+  M, E = x2d.shape
+  if packed_out is None:
+    packed_out = want_packed(M, E)
+  wd = decode_weight(w_packed) if M <= 32 else None
+  y = ops.rglru_step_(x2d, wd if wd is not None else w_packed, bias_x, bias_a,
+                      softplus_a, pos_flat, h, gate, wd is not None, packed_out)
+  return PackedRows(y, M, E) if packed_out else y
 
 
 def logits_argmax(x2d, embedding, soft_cap, return_logits):
+  a, ar = _a(x2d)
   wd = decode_weight(embedding) if x2d.shape[0] <= 32 else None
   if wd is not None:
-    return ops.logits_argmax(x2d, wd, soft_cap, return_logits, True)
-  return ops.logits_argmax(x2d, embedding, soft_cap, return_logits)
+    return ops.logits_argmax(a, wd, soft_cap, return_logits, True, ar)
+  return ops.logits_argmax(a, embedding, soft_cap, return_logits, False, ar)
 
 
 def gemm_logits(x2d, embedding, soft_cap):
+  a, ar = _a(x2d)
   wd = decode_weight(embedding) if x2d.shape[0] <= 32 else None
   if wd is not None:
-    return ops.gemm_logits(x2d, wd, soft_cap, True)
-  return ops.gemm_logits(x2d, embedding, soft_cap)
+    return ops.gemm_logits(a, wd, soft_cap, True, ar)
+  return ops.gemm_logits(a, embedding, soft_cap, False, ar)
 
 
-def rmsnorm(x2d, scale, eps=1e-6):
+def rmsnorm(x2d, scale, eps=1e-6, packed: bool = False):
+  """RMSNorm rows; packed=True (only for a GEMM consumer) returns PackedRows
+  when the rows qualify (want_packed)."""
+  if packed and want_packed(x2d.shape[0], x2d.shape[1]):
+    return PackedRows(ops.rmsnorm(x2d, scale, eps, True), x2d.shape[0],
+                      x2d.shape[1])
   return ops.rmsnorm(x2d, scale, eps)
+
+
+def local_attention_decode_(q, k, v, cache_k, cache_v, num_tokens, H):
+  """Decode attention step; the output is PackedRows for decode rows (it
+  only feeds proj_final)."""
+  B = q.shape[0]
+  hd = k.shape[-1]
+  pk = want_packed(B, H * hd)
+  out = ops.local_attention_decode_(q, k, v, cache_k, cache_v, num_tokens, H, pk)
+  return PackedRows(out, B, H * hd) if pk else out

@@ -14,8 +14,13 @@
 // decode_attn_kernel: one wave per sequence, 16 rows = the query heads,
 // keys = ring-buffer slots (positions of _compute_cache_mask) + the new key,
 // then the in-place slot update of _update_attention_cache.
+#include <cstdlib>
+#include <cstring>
 #include "common.hpp"
 #include "../../include/cadence_kernels.h"
+
+int vit_attention_lds_launch(const void* qkv, void* out, int64_t B, int64_t N,
+                             int64_t H, int64_t hd, void* stream);  // vit_attention.hip
 
 namespace {
 
@@ -235,7 +240,9 @@ struct DecodeArgs {
   int64_t new_rs;
   u16* ck; u16* cv;       // [B, W, hd]
   int32_t* num_tokens;    // [B]
-  u16* o;                 // [B, H*hd]
+  u16* o;                 // [B, H*hd] (ldo = H*hd) or packed rows (ldo = 0)
+  int64_t ldo;
+  int omt;                // ceil(B / 16) for packed rows
   int H, hd, W;
   float scale;
   float* parts;           // [B, NS, 32 + 16 * hd] fp32 split partials (NS > 1)
@@ -410,7 +417,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
 #pragma unroll
       for (int j = 0; j < NO; ++j) {
         const int d = dbase + j * 16 + (lane & 15);
-        a.o[(int64_t)b * a.H * a.hd + hrow * a.hd + d] = f2bf(o[j][r] * inv);
+        a.o[xoff(b, hrow * a.hd + d, a.ldo, a.omt)] = f2bf(o[j][r] * inv);
       }
     }
   } else {
@@ -472,7 +479,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
         acc[3] += __uint_as_float((uint32_t)(w1 >> 32)) * wgt;
       }
       const float inv = l > 0.0f ? 1.0f / l : 0.0f;
-      u16* dst = a.o + (int64_t)b * a.H * a.hd + q;
+      u16* dst = a.o + xoff(b, q, a.ldo, a.omt);
       const uint32_t lo = (uint32_t)f2bf(acc[0] * inv) | ((uint32_t)f2bf(acc[1] * inv) << 16);
       const uint32_t hi = (uint32_t)f2bf(acc[2] * inv) | ((uint32_t)f2bf(acc[3] * inv) << 16);
       *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
@@ -668,6 +675,16 @@ int cadence_vit_attention(const void* qkv, void* out, int64_t B, int64_t N,
                           int64_t H, int64_t hd, void* stream) {
   if (hd != 64 && hd != 72) return (int)hipErrorInvalidValue;
   if (B <= 0 || N <= 0) return 0;
+  // LDS-resident swapped-QK^T kernel (vit_attention.hip) for short sequences;
+  // CADENCE_VIT_ATTN=flash keeps the streaming flash kernel (A/B runs).
+  static const bool flash_only = [] {
+    const char* e = getenv("CADENCE_VIT_ATTN");
+    return e && strncmp(e, "flash", 5) == 0;
+  }();
+  if (!flash_only) {
+    const int rc = vit_attention_lds_launch(qkv, out, B, N, H, hd, stream);
+    if (rc >= 0) return rc;
+  }
   const int64_t D = H * hd;
   AttnArgs a{};
   const u16* base = static_cast<const u16*>(qkv);
@@ -705,18 +722,21 @@ int64_t cadence_local_attention_decode_workspace_bytes(int64_t B, int64_t hd) {
 int cadence_local_attention_decode(const void* q, const void* k_new,
                                    const void* v_new, void* cache_k,
                                    void* cache_v, int32_t* num_tokens,
-                                   void* out, int64_t B, int64_t H,
+                                   void* out, int64_t ld_out, int64_t B, int64_t H,
                                    int64_t hd, int64_t window, void* workspace,
                                    int64_t ws_bytes, int32_t* sems, void* stream) {
   if ((hd != 256 && hd != 128 && hd != 64) || H > 16)
     return (int)hipErrorInvalidValue;
+  if (ld_out == 0 && B > 32) return (int)hipErrorInvalidValue;   // packed rows
+  if (ld_out != 0 && ld_out < H * hd) return (int)hipErrorInvalidValue;
   if (B <= 0) return 0;
   const bool split = workspace && sems &&
                      ws_bytes >= cadence_local_attention_decode_workspace_bytes(B, hd);
   DecodeArgs a{static_cast<const u16*>(q), static_cast<const u16*>(k_new),
                static_cast<const u16*>(v_new), hd,
                static_cast<u16*>(cache_k), static_cast<u16*>(cache_v),
-               num_tokens, static_cast<u16*>(out), (int)H, (int)hd,
+               num_tokens, static_cast<u16*>(out), ld_out, (int)((B + 15) / 16),
+               (int)H, (int)hd,
                (int)window, 1.0f / sqrtf((float)hd),
                static_cast<float*>(workspace), sems};
   hipStream_t st = static_cast<hipStream_t>(stream);

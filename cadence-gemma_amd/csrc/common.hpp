@@ -105,4 +105,20 @@ CADENCE_DEV float wave_max(float v) {
   return v;
 }
 
+// Decode activation layout ("packed rows"; leading dimension 0 at the C ABI,
+// M <= 32 rows): the A-operand fragment order of mfma_f32_16x16x32_bf16, so
+// a decode GEMV's activation load is one contiguous 1 KiB per wave
+// instruction (row-major fragment loads touch 16 rows x 16 B per
+// instruction and halve the weight stream's rate).  mt = ceil(M / 16).
+//   Xp[((k / 32) * mt + m / 16) * 512 + (m % 16 + 16 * ((k % 32) / 8)) * 8 + k % 8]
+// Eight consecutive k of one row (k % 8 == 0) are one 16-B chunk.
+CADENCE_DEV int64_t xpk(int m, int k, int mt) {
+  return ((((int64_t)(k >> 5) * mt + (m >> 4)) * 64 + (m & 15) + ((k >> 3) & 3) * 16)
+          << 3) + (k & 7);
+}
+// Offset of row m, column k in either layout (ld == 0: packed).
+CADENCE_DEV int64_t xoff(int m, int k, int64_t ld, int mt) {
+  return ld ? (int64_t)m * ld + k : xpk(m, k, mt);
+}
+
 #define CADENCE_CHECK_LAUNCH() return (int)hipGetLastError()

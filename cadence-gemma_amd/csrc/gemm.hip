@@ -148,8 +148,9 @@ struct EpiGatedGelu {
   static constexpr bool kPaired = true;
   static constexpr bool kStaged = true;
   static constexpr bool kTile = false;
-  u16* out; int64_t ldo;
+  u16* out; int64_t ldo;        // ldo == 0: packed rows (M <= 32)
   const u16* bias_g; const u16* bias_u;
+  int mt;                        // ceil(M / 16)
   CADENCE_DEV float value2(int64_t, int f, float g, float u, int) const {
     // Einsum result is rounded, then `+ b` rounds again (layers.py:729).
     g = badd(rbf(g), bf2f(bias_g[f]));
@@ -157,7 +158,7 @@ struct EpiGatedGelu {
     return bmul(rbf(gelu_tanh(g)), u);
   }
   CADENCE_DEV void apply2(int64_t m, int f, float g, float u, int gg) const {
-    out[m * ldo + f] = f2bf(value2(m, f, g, u, gg));
+    out[xoff((int)m, f, ldo, mt)] = f2bf(value2(m, f, g, u, gg));
   }
   CADENCE_DEV float bias_at(bool up, int f, int) const {
     return bf2f((up ? bias_u : bias_g)[f]);
@@ -169,7 +170,7 @@ struct EpiGatedGelu {
     unpack8(u8, uv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) gv[i] = bmul(rbf(gelu_tanh(gv[i])), uv[i]);
-    st16(out + m * ldo + f, pack8(gv));
+    st16(out + xoff((int)m, f, ldo, mt), pack8(gv));
   }
 };
 
@@ -197,7 +198,8 @@ struct EpiRglruGates {
   // y = bf16(h) [* gate], state updated in place.
   float* h; int64_t ldh;
   const u16* gate; int64_t ldg;
-  u16* y_out; int64_t ldy;
+  u16* y_out; int64_t ldy;           // ldy == 0: packed rows (M <= 32)
+  int mt;                            // ceil(M / 16)
   // gx_pre / ga_pre are the bf16 BDL outputs (einsum rounded, + b rounded).
   CADENCE_DEV void chain(float gx_pre, float ga_pre, float xv, float sp,
                          bool reset, float& av, float& nx) const {
@@ -222,7 +224,7 @@ struct EpiRglruGates {
       *hp = hn;
       float y = rbf(hn);
       if (gate) y = bmul(y, bf2f(gate[m * ldg + e]));
-      y_out[m * ldy + e] = f2bf(y);
+      y_out[xoff((int)m, e, ldy, mt)] = f2bf(y);
       return;
     }
     a_out[m * ldo + e] = f2bf(av);
@@ -254,7 +256,7 @@ struct EpiRglruGates {
         y[i] = rbf(hn);
         if (gate) y[i] = bmul(y[i], gv[i]);
       }
-      st16(y_out + m * ldy + e, pack8(y));
+      st16(y_out + xoff((int)m, e, ldy, mt), pack8(y));
       return;
     }
     st16(a_out + m * ldo + e, pack8(av));
@@ -743,7 +745,10 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
 #pragma unroll
     for (int i = 0; i < MR; ++i) {
       const int m = i * 16 + (lane & 15);
-      xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + k + koff) : zero;
+      if (lda == 0)   // packed rows (common.hpp xpk): mt == MR here
+        xa[u][i] = ok ? ld16(A + ((((int64_t)(k >> 5) * MR + i) * 64 + lane) << 3)) : zero;
+      else
+        xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + k + koff) : zero;
     }
   }
   f32x4 acc[MR][NREP];
@@ -836,7 +841,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(
 #pragma unroll
       for (int i = 0; i < MR; ++i) {
         const int m = i * 16 + (lane & 15);
-        xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + k + koff) : zero;
+        if (lda == 0)   // packed rows, mt == MR
+          xa[u][i] = ok ? ld16(A + ((((int64_t)(k >> 5) * MR + i) * 64 + lane) << 3)) : zero;
+        else
+          xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + k + koff) : zero;
       }
     }
 #pragma unroll
@@ -1039,7 +1047,7 @@ __global__ __launch_bounds__(512) void reduce_rmsnorm_kernel(
       unpack8(sq[c], sc);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[c][i] = bmul(bmul(o[c][i], rs), badd(sc[i], 1.0f));
-      st16(nout + orow * ldn + n0, pack8(o[c]));
+      st16(nout + xoff((int)orow, n0, ldn, (M + 15) >> 4), pack8(o[c]));
     }
   }
 }
@@ -1123,6 +1131,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
   // ldw == 0: W is fragment-packed (see cadence_kernels.h), decode engines only
   const int packed = ldw == 0 ? 1 : 0;
   if (packed && (M > kSkinnyMaxM || N % 16 || K % 32)) return (int)hipErrorInvalidValue;
+  if (lda == 0 && (M > 32 || K % 32)) return (int)hipErrorInvalidValue;   // packed rows
   if (M > kSkinnyMaxM) {
     if (N % 64 || K % BK) return (int)hipErrorInvalidValue;
     if (use_legacy_tile() && N % 128 == 0) {
@@ -1205,7 +1214,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 5; }
+int cadence_abi_version(void) { return 6; }
 
 int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
                                      int64_t groups) {
@@ -1250,6 +1259,7 @@ int cadence_gemm_linear_rmsnorm(const void* A, int64_t lda, const void* W,
   if (M <= 0) return 0;
   if (N % 8 || ldo % 8 || ld_norm % 8 || (resid && ld_resid % 8))
     return (int)hipErrorInvalidValue;
+  if (ld_norm == 0 && (M > 32 || N % 32)) return (int)hipErrorInvalidValue;
   hipStream_t st = static_cast<hipStream_t>(stream);
   EpiLinear epi{static_cast<u16*>(out), ldo, static_cast<const u16*>(bias),
                 static_cast<const u16*>(resid), ld_resid, 0,
@@ -1295,9 +1305,10 @@ int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
                             int64_t M, int64_t F, int64_t K, void* workspace,
                             int64_t ws_bytes, void* stream) {
   if (F % 64 || (ldw != 0 && ldw < K)) return (int)hipErrorInvalidValue;
+  if (ldo == 0 && M > 32) return (int)hipErrorInvalidValue;   // packed rows
   EpiGatedGelu epi{static_cast<u16*>(out), ldo,
                    static_cast<const u16*>(bias_gate),
-                   static_cast<const u16*>(bias_up)};
+                   static_cast<const u16*>(bias_up), (int)((M + 15) / 16)};
   return launch_gemm(static_cast<const u16*>(A), lda,
                      static_cast<const u16*>(Wpacked), ldw, M, 2 * F, K, 1, 0, 0,
                      epi, workspace, ws_bytes, static_cast<hipStream_t>(stream));
@@ -1315,7 +1326,7 @@ int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
                     static_cast<const u16*>(bias_a),
                     static_cast<const u16*>(softplus_a), segment_pos,
                     static_cast<u16*>(a_out), static_cast<u16*>(nx_out), ldo,
-                    (int)bw, nullptr, 0, nullptr, 0, nullptr, 0};
+                    (int)bw, nullptr, 0, nullptr, 0, nullptr, 0, 1};
   return launch_gemm(static_cast<const u16*>(X), ldx,
                      static_cast<const u16*>(Wpacked), ldw, M, 2 * bw, bw, heads,
                      bw, 2 * bw * bw, epi, workspace, ws_bytes,
@@ -1330,13 +1341,14 @@ int cadence_rglru_step(const void* X, int64_t ldx, const void* Wpacked,
                        void* workspace, int64_t ws_bytes, void* stream) {
   if (bw % 64 || (ldw != 0 && ldw != bw) || !h || !y_out)
     return (int)hipErrorInvalidValue;
+  if (ldy == 0 && M > 32) return (int)hipErrorInvalidValue;   // packed rows
   EpiRglruGates epi{static_cast<const u16*>(X), ldx,
                     static_cast<const u16*>(bias_x),
                     static_cast<const u16*>(bias_a),
                     static_cast<const u16*>(softplus_a), segment_pos,
                     nullptr, nullptr, 0, (int)bw, h, heads * bw,
                     static_cast<const u16*>(gate), ldg, static_cast<u16*>(y_out),
-                    ldy};
+                    ldy, (int)((M + 15) / 16)};
   return launch_gemm(static_cast<const u16*>(X), ldx,
                      static_cast<const u16*>(Wpacked), ldw, M, 2 * bw, bw, heads,
                      bw, 2 * bw * bw, epi, workspace, ws_bytes,

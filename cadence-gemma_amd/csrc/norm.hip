@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   ss = wave_sum(ss);
   const float var = rbf(ss / (float)width);
   const float r = rbf(1.0f / sqrtf(rbf(var + eps)));
-  u16* orow = out + row * ldo;
+  const int mt = (int)((rows + 15) >> 4);   // ldo == 0: packed rows
 #pragma unroll
   for (int i = 0; i < RC; ++i) {
     const int c = lane * 8 + i * 512;
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
       unpack8(sv[i], sc);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = bmul(bmul(v[j], r), badd(sc[j], 1.0f));
-      st16(orow + c, pack8(v));
+      st16(out + xoff((int)row, c, ldo, mt), pack8(v));
     }
   }
 }
@@ -72,14 +72,14 @@ __global__ __launch_bounds__(256) void rmsnorm_wide_kernel(
   ss = wave_sum(ss);
   const float var = rbf(ss / (float)width);
   const float r = rbf(1.0f / sqrtf(rbf(var + eps)));
-  u16* orow = out + row * ldo;
+  const int mt = (int)((rows + 15) >> 4);   // ldo == 0: packed rows
   for (int c = lane * 8; c < width; c += 512) {
     float v[8], s[8];
     unpack8(ld16(xr + c), v);
     unpack8(ld16(scale + c), s);
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = bmul(bmul(v[i], r), badd(s[i], 1.0f));
-    st16(orow + c, pack8(v));
+    st16(out + xoff((int)row, c, ldo, mt), pack8(v));
   }
 }
 
@@ -208,6 +208,7 @@ int cadence_rmsnorm(const void* x, int64_t ldx, const void* scale, void* out,
                     int64_t ldo, int64_t rows, int64_t width, float eps,
                     void* stream) {
   if (width % 8 || ldx % 8 || ldo % 8) return (int)hipErrorInvalidValue;
+  if (ldo == 0 && (rows > 32 || width % 32)) return (int)hipErrorInvalidValue;
   if (rows <= 0) return 0;
   const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   hipStream_t st = static_cast<hipStream_t>(stream);

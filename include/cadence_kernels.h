@@ -23,6 +23,21 @@
  * stream is one contiguous range.  Requires N % 16 == 0, K % 32 == 0;
  * grouped launches pack each group separately.
  *
+ * Decode activation layout ("packed rows"): an ACTIVATION leading dimension
+ * of 0 (lda of a GEMM A operand, ldo / ld_norm / ldy / ld_out of the
+ * decode-side producers) means the M <= 32 rows are stored in the MFMA
+ * A-fragment order, mt = ceil(M / 16):
+ *   Xp[((k / 32) * mt + m / 16) * 512 + (m % 16 + 16 * ((k % 32) / 8)) * 8 + k % 8]
+ *       = X[m][k]
+ * so a decode GEMV loads 1 KiB of contiguous activations per wave
+ * instruction (row-major fragment loads halve its weight-stream rate).
+ * Requires K % 32 == 0; a packed buffer holds K * 16 * mt elements.
+ * Producers: cadence_rmsnorm (ldo = 0), cadence_gemm_linear_rmsnorm
+ * (ld_norm = 0), cadence_gemm_gated_gelu (ldo = 0), cadence_rglru_step
+ * (ldy = 0), cadence_local_attention_decode (ld_out = 0).  Consumers: the
+ * A operand of cadence_gemm_linear, cadence_gemm_linear_rmsnorm,
+ * cadence_gemm_gated_gelu, cadence_gemm_logits, cadence_logits_argmax.
+ *
  * The reference (`surakku/cadence-gemma`) has no native layer: each entry
  * point replaces a sequence of eager PyTorch ops (or timm ops) of the
  * reference Python path, cited per function.  The Python host
@@ -253,7 +268,7 @@ int64_t cadence_local_attention_decode_workspace_bytes(int64_t B, int64_t hd);
 int cadence_local_attention_decode(const void* q, const void* k_new,
                                    const void* v_new, void* cache_k,
                                    void* cache_v, int32_t* num_tokens,
-                                   void* out, int64_t B, int64_t H,
+                                   void* out, int64_t ld_out, int64_t B, int64_t H,
                                    int64_t hd, int64_t window, void* workspace,
                                    int64_t ws_bytes, int32_t* sems,
                                    void* stream);

@@ -132,6 +132,23 @@ def test_ops_have_no_cpu_fallback():
     torch.ops.cadence.rmsnorm(x, torch.zeros(8, dtype=torch.bfloat16), 1e-6)
 
 
+def test_packed_rows_layout_matches_header_formula():
+  """ops.pack_rows == the index formula of cadence_kernels.h ("Decode
+  activation layout"), for full and partial 16-row tiles."""
+  from cadence import ops
+  for m, k in ((32, 64), (17, 96), (5, 32)):
+    x = torch.arange(m * k, dtype=torch.float32).view(m, k).to(torch.bfloat16)
+    p = ops.pack_rows(x)
+    mt = -(-m // 16)
+    assert p.data.numel() == k * 16 * mt
+    for mm in range(m):
+      for kk in range(k):
+        idx = (((kk // 32) * mt + mm // 16) * 512 + (mm % 16 + 16 * ((kk % 32) // 8)) * 8
+               + kk % 8)
+        assert p.data[idx] == x[mm, kk], (m, k, mm, kk)
+    assert torch.equal(p.unpack(), x)
+
+
 def test_positions_and_sampler_prompt_layout():
   from cadence.sampler import prompt_positions
   pos = prompt_positions(torch.tensor([3, 5]), 5)

@@ -244,6 +244,8 @@ def test_gemm_linear_rmsnorm(dev, m, n, k):
   with torch.no_grad():
     norm.scale.copy_(rnd(n, scale=0.2, gen=g))
   out, nout = ops.linear_rmsnorm(a, w, bias, resid, norm)
+  if isinstance(nout, ops.PackedRows):     # decode rows: packed norm output
+    nout = nout.unpack()
   ref = ops.linear(a, w, bias, resid=resid)
   if m > 64:   # prefill: the same two kernels
     assert torch.equal(out, ref)
