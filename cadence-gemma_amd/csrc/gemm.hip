@@ -694,19 +694,23 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
   }
 }
 
-// Weight-streaming decode GEMM (M <= 32).  One workgroup = 16 output columns
-// (paired: 16 gate + 16 up packed columns) x one K split; wave w owns k-steps
-// w, w+8, ..., at most KSW of them, and issues ALL of its weight and
+// Weight-streaming decode GEMM (M <= 32).  One workgroup = NTW x 16 output
+// columns (paired: 16 gate + 16 up packed columns) x one K split; wave w owns
+// k-steps w, w+8, ..., at most KSW of them, and issues ALL of its weight and
 // activation loads before the first MFMA, so a workgroup waits for HBM once.
+// NTW = 2 reuses every activation fragment for two column tiles (the
+// activation loads, not the weight stream, bound the NTW = 1 form on the
+// wide shapes); fragment-packed weights are read once, non-temporal.
 // parts == nullptr: fixed-order LDS reduction + fused epilogue.  Otherwise
 // raw fp32 partials go to parts[split][M][N] for splitk_reduce_kernel.
-template <int MS, int KSW, class Epi>
+template <int MS, int KSW, int NTW, class Epi>
 __global__ __launch_bounds__(512) void gemm_stream_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
     int64_t ldw, int M, int N, int K, int klen, int64_t a_goff, int64_t w_goff,
     float* __restrict__ parts, Epi epi, int packed) {
   constexpr int MR = MS / 16;
-  constexpr int NREP = Epi::kPaired ? 2 : 1;
+  static_assert(!Epi::kPaired || NTW == 1, "paired epilogues pair gate/up tiles");
+  constexpr int NREP = Epi::kPaired ? 2 : NTW;
   __shared__ float red[8][MS * 16 * NREP];
   const int g = blockIdx.z;
   A += g * a_goff;
@@ -718,7 +722,8 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
     col[0] = grp * 64 + half * 16;
     col[NREP - 1] = grp * 64 + 32 + half * 16;
   } else {
-    col[0] = blockIdx.x * 16;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) col[t] = (blockIdx.x * NTW + t) * 16;
   }
   const int koff = 8 * (lane >> 4);
   const int kbeg = blockIdx.y * klen;
@@ -732,7 +737,7 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
 #pragma unroll
     for (int j = 0; j < NREP; ++j)
       if (packed)   // fragment-packed [N/16][K/32][64 lanes][8]: 1 KiB per load
-        wb[u][j] = ok ? ld16(W + (((int64_t)(col[j] >> 4) * (K >> 5) + (k >> 5)) * 64 + lane) * 8)
+        wb[u][j] = ok ? ld16_nt(W + (((int64_t)(col[j] >> 4) * (K >> 5) + (k >> 5)) * 64 + lane) * 8)
                       : zero;
       else
         wb[u][j] = ok ? ld16(W + (int64_t)(col[j] + (lane & 15)) * ldw + k + koff)
@@ -793,7 +798,8 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
       const int grp = blockIdx.x >> 1, half = blockIdx.x & 1;
       epi.apply2(m, grp * 32 + half * 16 + c, v[0], v[NREP - 1], g);
     } else {
-      epi.apply(m, col[0] + c, v[0], g);
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) epi.apply(m, col[j] + c, v[j], g);
     }
   }
 }
@@ -836,7 +842,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         wb[u][j] = !ok ? zero
-                   : packed ? ld16(W + (((int64_t)((n0 >> 4) + j) * (K >> 5) + (k >> 5)) * 64 + lane) * 8)
+                   : packed ? ld16_nt(W + (((int64_t)((n0 >> 4) + j) * (K >> 5) + (k >> 5)) * 64 + lane) * 8)
                             : ld16(W + (int64_t)(n0 + j * 16 + (lane & 15)) * ldw + k + koff);
 #pragma unroll
       for (int i = 0; i < MR; ++i) {
@@ -1100,24 +1106,30 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
                    int64_t M, int64_t N, int64_t K, int64_t groups,
                    int64_t a_goff, int64_t w_goff, const Epi& epi, int ksw,
                    int splits, float* parts, int packed, hipStream_t st) {
-  const unsigned nblk = (unsigned)(Epi::kPaired ? N / 32 : N / 16);
+  // two column tiles per workgroup when that still leaves >= 150 workgroups
+  // (cold-weight sweep, tools/gemv_lab.py: xy 12.7 -> 8.9 us, down 18.6 -> 13)
+  const int ntw = (!Epi::kPaired && ksw == 10 && N % 32 == 0 &&
+                   (N / 32) * splits * groups >= 150) ? 2 : 1;
+  const unsigned nblk = (unsigned)(Epi::kPaired ? N / 32 : N / 16 / ntw);
   const int64_t ks = K / 32;
   const int klen = (int)((ks + splits - 1) / splits) * 32;
   dim3 grid(nblk, (unsigned)splits, (unsigned)groups);
-#define CADENCE_STREAM(MS_, KSW_)                                               \
-  hipLaunchKernelGGL((gemm_stream_kernel<MS_, KSW_, Epi>), grid, dim3(512), 0, st, \
-                     A, lda, W, ldw, (int)M, (int)N, (int)K, klen, a_goff,      \
+#define CADENCE_STREAM(MS_, KSW_, NTW_)                                          \
+  hipLaunchKernelGGL((gemm_stream_kernel<MS_, KSW_, NTW_, Epi>), grid, dim3(512), \
+                     0, st, A, lda, W, ldw, (int)M, (int)N, (int)K, klen, a_goff, \
                      w_goff, parts, epi, packed)
   if (M <= 16) {
-    if (ksw == 1) CADENCE_STREAM(16, 1);
-    else if (ksw == 2) CADENCE_STREAM(16, 2);
-    else if (ksw == 4) CADENCE_STREAM(16, 4);
-    else CADENCE_STREAM(16, 10);
+    if (ksw == 1) CADENCE_STREAM(16, 1, 1);
+    else if (ksw == 2) CADENCE_STREAM(16, 2, 1);
+    else if (ksw == 4) CADENCE_STREAM(16, 4, 1);
+    else if (ntw == 2) { if constexpr (!Epi::kPaired) CADENCE_STREAM(16, 10, 2); }
+    else CADENCE_STREAM(16, 10, 1);
   } else {
-    if (ksw == 1) CADENCE_STREAM(32, 1);
-    else if (ksw == 2) CADENCE_STREAM(32, 2);
-    else if (ksw == 4) CADENCE_STREAM(32, 4);
-    else CADENCE_STREAM(32, 10);
+    if (ksw == 1) CADENCE_STREAM(32, 1, 1);
+    else if (ksw == 2) CADENCE_STREAM(32, 2, 1);
+    else if (ksw == 4) CADENCE_STREAM(32, 4, 1);
+    else if (ntw == 2) { if constexpr (!Epi::kPaired) CADENCE_STREAM(32, 10, 2); }
+    else CADENCE_STREAM(32, 10, 1);
   }
 #undef CADENCE_STREAM
 }

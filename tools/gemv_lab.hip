@@ -28,7 +28,7 @@ __global__ __launch_bounds__(512) void read_kernel(const uint4* __restrict__ p,
 // grid (N/16/NTW, S); NW waves; wave w owns k-steps kb + w + NW*u, u < KSW,
 // for NTW adjacent 16-column tiles (the A fragments are reused NTW times).
 // NOA: ablation, no activation loads (A fragment = constant).
-template <int NW, int KSW, int NTW, int AMODE>
+template <int NW, int KSW, int NTW, int AMODE, bool NT = false>
 __global__ __launch_bounds__(NW * 64) void gemv_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int M,
     int N, int K, float* __restrict__ parts, int* __restrict__ cnt,
@@ -51,7 +51,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(
     const int k = kb + wave + NW * u;
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
-      wb[u][t] = k < ke ? ld16(Wp + (((int64_t)(grp * NTW + t) * kst + k) * 64 + lane) * 8)
+      wb[u][t] = k < ke ? (NT ? ld16_nt(Wp + (((int64_t)(grp * NTW + t) * kst + k) * 64 + lane) * 8)
+                              : ld16(Wp + (((int64_t)(grp * NTW + t) * kst + k) * 64 + lane) * 8))
                         : zero;
   }
   if constexpr (kLds) {
@@ -185,15 +186,20 @@ int lab_gemv(const void* A, int64_t lda, const void* Wp, int M, int N, int K,
   const dim3 grid(N / 16 / ntw, splits);
   hipStream_t st = (hipStream_t)stream;
 #define L1(NW_, KSW_, NTW_, AM_)                                                   \
-  if (nw == NW_ && ksw == KSW_ && ntw == NTW_ && amode == AM_) {                   \
-    hipLaunchKernelGGL((gemv_kernel<NW_, KSW_, NTW_, AM_>), grid, dim3(NW_ * 64), 0, \
-                       st, (const u16*)A, lda, (const u16*)Wp, M, N, K, parts, cnt, \
-                       (const u16*)bias, (u16*)out, ldo);                          \
+  if (nw == NW_ && ksw == KSW_ && ntw == NTW_ && (amode & 15) == AM_) {            \
+    if (amode & 16)                                                                \
+      hipLaunchKernelGGL((gemv_kernel<NW_, KSW_, NTW_, AM_, true>), grid,          \
+                         dim3(NW_ * 64), 0, st, (const u16*)A, lda, (const u16*)Wp, \
+                         M, N, K, parts, cnt, (const u16*)bias, (u16*)out, ldo);   \
+    else                                                                           \
+      hipLaunchKernelGGL((gemv_kernel<NW_, KSW_, NTW_, AM_, false>), grid,         \
+                         dim3(NW_ * 64), 0, st, (const u16*)A, lda, (const u16*)Wp, \
+                         M, N, K, parts, cnt, (const u16*)bias, (u16*)out, ldo);   \
     return (int)hipGetLastError();                                                 \
   }
-#define L(NW_, KSW_, NTW_) L1(NW_, KSW_, NTW_, 0) L1(NW_, KSW_, NTW_, 1) L1(NW_, KSW_, NTW_, 2) L1(NW_, KSW_, NTW_, 3)
+#define L(NW_, KSW_, NTW_) L1(NW_, KSW_, NTW_, 0) L1(NW_, KSW_, NTW_, 2)
   L(8, 10, 1) L(8, 4, 2) L(8, 5, 2) L(4, 5, 2) L(4, 5, 4) L(8, 5, 4) L(16, 2, 2) L(4, 10, 2) L(8, 10, 2)
-  L(4, 10, 1) L(8, 5, 1) L(4, 20, 1)
+  L(4, 10, 1) L(8, 5, 1) L(4, 20, 1) L(8, 2, 1) L(8, 4, 1) L(16, 5, 1) L(16, 1, 1)
 #undef L1
 #undef L
   return 1;
