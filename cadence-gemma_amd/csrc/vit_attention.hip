@@ -15,6 +15,8 @@
 // Replaces timm `Attention.forward` (F.scaled_dot_product_attention,
 // bidirectional, scale hd^-1/2) called from recurrentgemma/vit/dino_siglip.py
 // :85-86,149-151 (timm not vendored).
+#include <cstdio>
+#include <cstdlib>
 #include "common.hpp"
 #include "../../include/cadence_kernels.h"
 
@@ -26,11 +28,12 @@ CADENCE_DEV int kswz(int ch, int row) {
 }
 
 // HDK: head dim padded to a multiple of 32 (QK^T k-steps); HDV: padded to 16
-// (O^T row tiles); NPMAX: LDS capacity in keys (multiple of 32); NW waves.
-template <int HDK, int HDV, int NPMAX, int NW>
+// (O^T row tiles); NPMAX: LDS capacity in keys (multiple of 32); NW waves;
+// QT query tiles per wave pass.
+template <int HDK, int HDV, int NPMAX, int NW, int QT>
 __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
     const u16* __restrict__ qkv, u16* __restrict__ out, int N, int H, int hd,
-    float scale_log2) {
+    float scale_log2, int dbg) {
   constexpr int CPR = HDK / 8;        // 16-B chunks per K row
   constexpr int KS = HDK / 32;
   constexpr int NDT = HDV / 16;
@@ -53,14 +56,14 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
   const uint4 zero = make_uint4(0, 0, 0, 0);
 
   // K -> LDS, zero-filled past N and past hd
-  for (int c = tid; c < np * CPR; c += NW * 64) {
+  for (int c = (dbg == 2 ? 1 << 30 : tid); c < np * CPR; c += NW * 64) {
     const int key = c / CPR, ch = c % CPR;
     uint4 v = zero;
     if (key < N && ch * 8 < hd) v = ld16(kb + key * rs + ch * 8);
     kimg[key * CPR + kswz<CPR>(ch, key)] = v;
   }
   // V^T -> LDS: one item = 4 keys x 8 dims, written as 8 runs of 4 keys
-  for (int it = tid; it < (np / 4) * VCH; it += NW * 64) {
+  for (int it = (dbg == 2 ? 1 << 30 : tid); it < (np / 4) * VCH; it += NW * 64) {
     const int kq = it / VCH, dc = it % VCH;
     uint4 v[4];
 #pragma unroll
@@ -84,81 +87,151 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
   __syncthreads();
 
   const int g = lane >> 4, c16 = lane & 15;
-  const int nqt = (N + 15) >> 4;
-  for (int qt = wave; qt < nqt; qt += NW) {
-    const int q = qt * 16 + c16;
-    bf16x8 qf[KS];
+  const int nqt = dbg == 1 ? 0 : (N + 15) >> 4;
+  // QT query tiles per pass share every K / V^T fragment read and give the
+  // wave QT independent S -> softmax -> PV chains to interleave.
+  // Q fragments: unconditional loads from clamped addresses (a branch around
+  // a load costs a full vmcnt(0) round trip), the next pass's prefetched
+  // while this one computes.
+  auto load_q = [&](int qt0, uint4 (&dst)[QT][KS]) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int d = ks * 32 + 8 * g;
-      qf[ks] = __builtin_bit_cast(bf16x8, (q < N && d < hd) ? ld16(qb + q * rs + d) : zero);
+    for (int u = 0; u < QT; ++u) {
+      const int qq = min((qt0 + u) * 16 + c16, N - 1);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        dst[u][ks] = ld16(qb + qq * rs + min(ks * 32 + 8 * g, hd - 8));
     }
-    f32x4 o[NDT];
+  };
+  uint4 qn[QT][KS];
+  load_q(wave * QT, qn);
+  for (int qt0 = wave * QT; qt0 < nqt; qt0 += NW * QT) {
+    int q[QT];
+    bf16x8 qf[QT][KS];
 #pragma unroll
-    for (int j = 0; j < NDT; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m = -INFINITY, l = 0.0f;
-    for (int c0 = 0; c0 < np; c0 += 32) {
-      f32x4 s[2];
+    for (int u = 0; u < QT; ++u) {
+      q[u] = (qt0 + u) * 16 + c16;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < KS; ++ks) {
+        const bool ok = q[u] < N && ks * 32 + 8 * g < hd;
+        qf[u][ks] = __builtin_bit_cast(bf16x8, ok ? qn[u][ks] : zero);
+      }
+    }
+    load_q(min(qt0 + NW * QT, nqt - 1), qn);
+    f32x4 o[QT][NDT];
+    float m[QT], l[QT];
+#pragma unroll
+    for (int u = 0; u < QT; ++u) {
+      m[u] = -INFINITY;
+      l[u] = 0.0f;
+#pragma unroll
+      for (int j = 0; j < NDT; ++j) o[u][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // 64-key chunks (the last one may be a 32-key tail), masking only where
+    // a chunk runs past N, the scale folded into one FMA before exp2, and the
+    // running max updated only when it grows by more than 2^8 (deferred
+    // rescale: P <= 256 is exact enough in bf16, l and O stay fp32).
+    constexpr float kThr = 8.0f;
+    for (int c0 = 0; c0 < np; c0 += 64) {
+      const bool two = c0 + 32 >= np;        // 32-key tail chunk
+      const bool mask = c0 + 64 > N;
+      f32x4 s[QT][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int u = 0; u < QT; ++u) s[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (t >= 2 && two) continue;
         const int kr = c0 + 16 * t + c16;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const bf16x8 kf = __builtin_bit_cast(bf16x8, kimg[kr * CPR + kswz<CPR>(ks * 4 + g, kr)]);
-          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[t], 0, 0, 0);
+#pragma unroll
+          for (int u = 0; u < QT; ++u)
+            s[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[u][ks], s[u][t], 0, 0, 0);
         }
       }
-      float p[8];
-      float cm = -INFINITY;
+      bf16x8 pf[QT][2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int u = 0; u < QT; ++u) {
+        if (mask) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = c0 + 16 * t + 4 * g + r;
-          const float v = key < N ? s[t][r] * scale_log2 : -INFINITY;
-          p[t * 4 + r] = v;
-          cm = fmaxf(cm, v);
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (c0 + 16 * t + 4 * g + r >= N) s[u][t][r] = -INFINITY;
         }
-      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
-      const float mn = fmaxf(m, cm);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);   // m = -inf: 0
-      float ps = 0.0f;
-      uint32_t pk[4];
+        float smax = fmaxf(fmaxf(s[u][0][0], s[u][0][1]), fmaxf(s[u][0][2], s[u][0][3]));
 #pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        const float e0 = __builtin_amdgcn_exp2f(p[j] - mn);
-        const float e1 = __builtin_amdgcn_exp2f(p[j + 1] - mn);
-        ps += e0 + e1;
-        pk[j >> 1] = (uint32_t)f2bf(e0) | ((uint32_t)f2bf(e1) << 16);
+        for (int t = 1; t < 4; ++t) {
+          if (t >= 2 && two) continue;
+          smax = fmaxf(smax, fmaxf(fmaxf(s[u][t][0], s[u][t][1]),
+                                   fmaxf(s[u][t][2], s[u][t][3])));
+        }
+        smax = fmaxf(smax, __shfl_xor(smax, 16, 64));
+        smax = fmaxf(smax, __shfl_xor(smax, 32, 64));
+        const float mt = smax * scale_log2;
+        const bool need = mt > m[u] + kThr;
+        if (__any(need)) {
+          const float mn = need ? mt : m[u];
+          const float alpha = __builtin_amdgcn_exp2f(m[u] - mn);   // m = -inf: 0
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[u][dt][r] *= alpha;
+          l[u] *= alpha;
+          m[u] = mn;
+        }
+        const float nm = -m[u];
+        float ps = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          uint32_t pk[4] = {0u, 0u, 0u, 0u};
+          if (!(kk == 1 && two)) {
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+              const int t = 2 * kk + (j >> 2), r = j & 3;
+              const float e0 = __builtin_amdgcn_exp2f(fmaf(s[u][t][r], scale_log2, nm));
+              const float e1 = __builtin_amdgcn_exp2f(fmaf(s[u][t][r + 1], scale_log2, nm));
+              ps += e0 + e1;
+              pk[j >> 1] = (uint32_t)f2bf(e0) | ((uint32_t)f2bf(e1) << 16);
+            }
+          }
+          pf[u][kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+        }
+        l[u] += ps;
       }
-      l = l * alpha + ps;
-      m = mn;
-      const bf16x8 pf = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
+      for (int kk = 0; kk < 2; ++kk) {
+        if (kk == 1 && two) continue;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;
-        const u16* vr = vt + (dt * 16 + c16) * VTS + c0 + 4 * g;
-        const uint2 lo = *reinterpret_cast<const uint2*>(vr);
-        const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
-        const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+        for (int dt = 0; dt < NDT; ++dt) {
+          const u16* vr = vt + (dt * 16 + c16) * VTS + c0 + 32 * kk + 4 * g;
+          const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+          const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+#pragma unroll
+          for (int u = 0; u < QT; ++u)
+            o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[u][kk], o[u][dt], 0, 0, 0);
+        }
       }
     }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    const float inv = 1.0f / l;
-    if (q < N) {
-      u16* orow = out + ((int64_t)b * N + q) * D + (int64_t)h * hd;
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const int d0 = dt * 16 + 4 * g;
-        if (d0 < hd) {
-          const uint32_t lo = (uint32_t)f2bf(o[dt][0] * inv) | ((uint32_t)f2bf(o[dt][1] * inv) << 16);
-          const uint32_t hi = (uint32_t)f2bf(o[dt][2] * inv) | ((uint32_t)f2bf(o[dt][3] * inv) << 16);
-          *reinterpret_cast<uint2*>(orow + d0) = make_uint2(lo, hi);
+    for (int u = 0; u < QT; ++u) {
+      float lt = l[u];
+      lt += __shfl_xor(lt, 16, 64);
+      lt += __shfl_xor(lt, 32, 64);
+      const float inv = 1.0f / lt;
+      if (q[u] < N) {
+        u16* orow = out + ((int64_t)b * N + q[u]) * D + (int64_t)h * hd;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int d0 = dt * 16 + 4 * g;
+          if (d0 < hd) {
+            const uint32_t lo = (uint32_t)f2bf(o[u][dt][0] * inv) |
+                                ((uint32_t)f2bf(o[u][dt][1] * inv) << 16);
+            const uint32_t hi = (uint32_t)f2bf(o[u][dt][2] * inv) |
+                                ((uint32_t)f2bf(o[u][dt][3] * inv) << 16);
+            *reinterpret_cast<uint2*>(orow + d0) = make_uint2(lo, hi);
+          }
         }
       }
     }
@@ -170,24 +243,47 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
 // LDS-resident form for the sequence lengths it covers (224-px towers:
 // DINO N = 261, SigLIP N = 256); returns -1 when the caller should use the
 // streaming flash kernel instead (longer sequences).
-__attribute__((visibility("hidden"))) int vit_attention_lds_launch(const void* qkv, void* out, int64_t B, int64_t N,
-                              int64_t H, int64_t hd, void* stream) {
+__attribute__((visibility("hidden"))) int vit_attention_lds_launch(
+    const void* qkv, void* out, int64_t B, int64_t N, int64_t H, int64_t hd,
+    void* stream) {
+  // CADENCE_VIT_ATTN_CFG = "<waves>x<query tiles>" (A/B sweeps; read once)
+  static const int cfg = [] {
+    const char* e = getenv("CADENCE_VIT_ATTN_CFG");
+    if (!e) return 0;
+    int nw = 0, qt = 0;
+    if (sscanf(e, "%dx%d", &nw, &qt) != 2) return 0;
+    return nw * 10 + qt;
+  }();
+  static const int dbg = [] {   // CADENCE_VIT_ATTN_DBG: 1 staging only, 2 compute only
+    const char* e = getenv("CADENCE_VIT_ATTN_DBG");
+    return e ? atoi(e) : 0;
+  }();
   const float sl2 = 1.4426950408889634f / sqrtf((float)hd);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)H, (unsigned)B);
   const u16* in = static_cast<const u16*>(qkv);
   u16* o = static_cast<u16*>(out);
+#define VA(HDK_, HDV_, NP_, NW_, QT_)                                                \
+  hipLaunchKernelGGL((vit_attn_kernel<HDK_, HDV_, NP_, NW_, QT_>), grid, dim3(NW_ * 64), \
+                     0, st, in, o, (int)N, (int)H, (int)hd, sl2, dbg)
+#define VSEL(HDK_, HDV_, NP_, DEF_NW, DEF_QT)                                        \
+  switch (cfg ? cfg : DEF_NW * 10 + DEF_QT) {                                        \
+    case 41: VA(HDK_, HDV_, NP_, 4, 1); break;                                       \
+    case 42: VA(HDK_, HDV_, NP_, 4, 2); break;                                       \
+    case 81: VA(HDK_, HDV_, NP_, 8, 1); break;                                       \
+    case 82: VA(HDK_, HDV_, NP_, 8, 2); break;                                       \
+    default: return -1;                                                              \
+  }
   if (hd == 64 && N <= 288) {
-    hipLaunchKernelGGL((vit_attn_kernel<64, 64, 288, 4>), grid, dim3(256), 0, st, in, o,
-                       (int)N, (int)H, (int)hd, sl2);
+    VSEL(64, 64, 288, 8, 1)
   } else if (hd == 72 && N <= 256) {
-    hipLaunchKernelGGL((vit_attn_kernel<96, 80, 256, 8>), grid, dim3(512), 0, st, in, o,
-                       (int)N, (int)H, (int)hd, sl2);
+    VSEL(96, 80, 256, 8, 1)
   } else if (hd == 72 && N <= 288) {
-    hipLaunchKernelGGL((vit_attn_kernel<96, 80, 288, 8>), grid, dim3(512), 0, st, in, o,
-                       (int)N, (int)H, (int)hd, sl2);
+    VSEL(96, 80, 288, 8, 1)
   } else {
     return -1;
   }
+#undef VSEL
+#undef VA
   return (int)hipGetLastError();
 }
