@@ -522,7 +522,34 @@ __global__ __launch_bounds__(256, 2) void gemm_tile_kernel(
 typedef const void __attribute__((address_space(1)))* gptr_t;
 typedef void __attribute__((address_space(3)))* lptr_t;
 
-template <class Epi>
+// 8-phase schedule (P8, K % 128 == 0).  The two LDS buffers (even / odd
+// K-tile) are each cut into four 16 KiB half-tiles by the wave sub-tile they
+// feed: A-h0 = rows {0..63, 128..191} (first 64 rows of each M-wave), A-h1 =
+// {64..127, 192..255}, B-h0 / B-h1 = first / second 32 columns of each
+// N-wave.  An iteration computes two K-tiles in 8 phases; phase p computes
+// one 64x32 quadrant of the wave tile (16 MFMAs) from fragments read at the
+// phase start and stages ONE half-tile (2 LDS-DMA instructions per lane):
+//   p  reads            quadrant    stages
+//   1  E.A-h0, E.B-h0   (m0, n0)    O.A-h1 <- K-tile 2i+1
+//   2  E.B-h1           (m0, n1)    E.A-h0 <- 2i+2
+//   3  E.A-h1           (m1, n1)    E.B-h0 <- 2i+2
+//   4  -                (m1, n0)    E.B-h1 <- 2i+2; vmcnt(6) retires O
+//   5  O.A-h0, O.B-h0   (m0, n0)    E.A-h1 <- 2i+2
+//   6  O.B-h1           (m0, n1)    O.A-h0 <- 2i+3
+//   7  O.A-h1           (m1, n1)    O.B-h0 <- 2i+3
+//   8  -                (m1, n0)    O.B-h1 <- 2i+3; vmcnt(6) retires E
+// Every half-tile is restaged >= 1 phase after its last read (a phase's
+// reads feed its own MFMAs, so they are retired by the phase-end barrier) and
+// read >= 1 phase after the counted vmcnt that retires it, so three
+// half-tiles of DMA stay in flight across every barrier (no vmcnt(0) in the
+// loop; raw s_barrier, since __syncthreads() would drain the DMA).
+CADENCE_DEV void p8_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <class Epi, bool P8>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
     int64_t ldw, int M, int N, int K, int64_t a_goff, int64_t w_goff,
@@ -553,10 +580,128 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
 
-  // DMA mapping: wave w moves pieces 8w..8w+7 of the 64 pieces of a K tile
-  // (pieces 0..31 = A rows, 32..63 = W rows); lane l of a piece lands at LDS
-  // row 8*piece + l/8, slot l%8, so it loads source chunk (l%8) ^ (l/8).
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // DMA mapping: lane l of an 8-row piece lands at LDS row 8*piece + l/8,
+  // slot l%8, so it loads source chunk (l%8) ^ (l/8) (XOR swizzle).
   const int src_chunk = (lane & 7) ^ (lane >> 3);
+  if constexpr (P8) {
+    constexpr int HT = 128 * 8;                 // uint4 per half-tile
+    // wave w moves pieces 2w, 2w+1 (8 rows each) of every half-tile
+    const u16* sa[2][2];
+    const u16* sb[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const int r = (2 * wave + pc) * 8 + (lane >> 3);   // half-tile row
+        const int gm = min(m0 + (r >> 6) * 128 + h * 64 + (r & 63), M - 1);
+        const int gn = min(n0 + (r >> 5) * 64 + h * 32 + (r & 31), N - 1);
+        sa[h][pc] = A + (int64_t)gm * lda + src_chunk * 8;
+        sb[h][pc] = W + (int64_t)gn * ldw + src_chunk * 8;
+      }
+    auto stage = [&](int buf, int kind, const u16* p0, const u16* p1, int k0) {
+      uint4* dst = &smem[(buf * 4 + kind) * HT + (2 * wave) * 64];
+      __builtin_amdgcn_global_load_lds((gptr_t)(p0 + k0), (lptr_t)dst, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)(p1 + k0), (lptr_t)(dst + 64), 16, 0, 0);
+    };
+    const int xr = lane & 7;   // row & 7 of every fragment row this lane reads
+    bf16x8 af[4][2], b0[2][2], b1[2][2];
+    auto readA = [&](int buf, int mh) {
+      const uint4* base = &smem[(buf * 4 + mh) * HT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          af[i][ks] = __builtin_bit_cast(
+              bf16x8, base[(wm * 64 + i * 16 + (lane & 15)) * 8 +
+                           ((ks * 4 + (lane >> 4)) ^ xr)]);
+    };
+    auto readB = [&](int buf, int nh, bf16x8 (&bf)[2][2]) {
+      const uint4* base = &smem[(buf * 4 + 2 + nh) * HT];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          bf[j][ks] = __builtin_bit_cast(
+              bf16x8, base[(wn * 32 + j * 16 + (lane & 15)) * 8 +
+                           ((ks * 4 + (lane >> 4)) ^ xr)]);
+    };
+    auto mma = [&](int mh, int nh, const bf16x8 (&bf)[2][2]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                af[i][ks], bf[j][ks], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    const int nk = K / BK;
+    // prologue: even <- tile 0 (all four), odd <- tile 1 (A-h0, B-h0, B-h1)
+    stage(0, 0, sa[0][0], sa[0][1], 0);
+    stage(0, 1, sa[1][0], sa[1][1], 0);
+    stage(0, 2, sb[0][0], sb[0][1], 0);
+    stage(0, 3, sb[1][0], sb[1][1], 0);
+    stage(1, 0, sa[0][0], sa[0][1], BK);
+    stage(1, 2, sb[0][0], sb[0][1], BK);
+    stage(1, 3, sb[1][0], sb[1][1], BK);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    p8_barrier();
+    for (int it = 0; it < nk / 2; ++it) {
+      const int kO1 = (2 * it + 1) * BK, kE = (2 * it + 2) * BK, kO = (2 * it + 3) * BK;
+      const bool more = 2 * it + 2 < nk;         // tiles 2i+2 and 2i+3 exist
+      // phase 1
+      readA(0, 0);
+      readB(0, 0, b0);
+      stage(1, 1, sa[1][0], sa[1][1], kO1);
+      mma(0, 0, b0); p8_barrier();
+      // phase 2
+      readB(0, 1, b1);
+      if (more) stage(0, 0, sa[0][0], sa[0][1], kE);
+      mma(0, 1, b1); p8_barrier();
+      // phase 3
+      readA(0, 1);
+      if (more) stage(0, 2, sb[0][0], sb[0][1], kE);
+      mma(1, 1, b1); p8_barrier();
+      // phase 4
+      if (more) {
+        stage(0, 3, sb[1][0], sb[1][1], kE);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      mma(1, 0, b0); p8_barrier();
+      // phase 5
+      readA(1, 0);
+      readB(1, 0, b0);
+      if (more) stage(0, 1, sa[1][0], sa[1][1], kE);
+      mma(0, 0, b0); p8_barrier();
+      // phase 6
+      readB(1, 1, b1);
+      if (more) stage(1, 0, sa[0][0], sa[0][1], kO);
+      mma(0, 1, b1); p8_barrier();
+      // phase 7
+      readA(1, 1);
+      if (more) stage(1, 2, sb[0][0], sb[0][1], kO);
+      mma(1, 1, b1); p8_barrier();
+      // phase 8
+      if (more) {
+        stage(1, 3, sb[1][0], sb[1][1], kO);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      mma(1, 0, b0); p8_barrier();
+    }
+  } else {
+  // 2-buffer schedule: wave w moves pieces 8w..8w+7 of the 64 pieces of a
+  // K tile (pieces 0..31 = A rows, 32..63 = W rows).
   const u16* src[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -578,12 +723,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
           (lptr_t)(&smem[(buf * ROWS + piece * 8) * 8]), 16, 0, 0);
     }
   };
-
-  f32x4 acc[MR][NR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BK;
   const int sw = lane & 7;  // (row & 7) of every row this lane reads
@@ -613,6 +752,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
       }
     }
     __syncthreads();   // waits this wave's DMA (vmcnt) + all waves' reads
+  }
   }
 
   const int mbase = m0 + wm * 128, nbase = n0 + wn * 64;
@@ -1156,11 +1296,21 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
     }
     const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
     dim3 grid((unsigned)tiles, (unsigned)groups);
+    // 8-phase pipeline when K splits into pairs of 64-deep tiles
+    // (CADENCE_GEMM_P8=0 keeps the 2-buffer schedule for A/B runs)
+    static const bool p8_off = [] {
+      const char* e = getenv("CADENCE_GEMM_P8");
+      return e && e[0] == '0';
+    }();
+    const bool p8 = !p8_off && K % (2 * BK) == 0;
     if constexpr (std::is_same_v<Epi, EpiLinear>) {
 #define CADENCE_BIG_ACT(ACT_)                                                          \
-  hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>>), grid, dim3(512), 0, st, A, \
-                     lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff,            \
-                     EpiLinearA<ACT_>{epi})
+  if (p8) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, true>), grid, dim3(512), \
+                             0, st, A, lda, W, ldw, (int)M, (int)N, (int)K, a_goff,     \
+                             w_goff, EpiLinearA<ACT_>{epi});                            \
+  else hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, false>), grid, dim3(512),  \
+                          0, st, A, lda, W, ldw, (int)M, (int)N, (int)K, a_goff,        \
+                          w_goff, EpiLinearA<ACT_>{epi})
       switch (epi.act) {
         case 0: CADENCE_BIG_ACT(0); break;
         case 1: CADENCE_BIG_ACT(1); break;
@@ -1169,8 +1319,11 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
         default: return (int)hipErrorInvalidValue;
       }
 #undef CADENCE_BIG_ACT
+    } else if (p8) {
+      hipLaunchKernelGGL((gemm_big_kernel<Epi, true>), grid, dim3(512), 0, st, A, lda, W,
+                         ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
     } else {
-      hipLaunchKernelGGL((gemm_big_kernel<Epi>), grid, dim3(512), 0, st, A, lda, W,
+      hipLaunchKernelGGL((gemm_big_kernel<Epi, false>), grid, dim3(512), 0, st, A, lda, W,
                          ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
     }
     return (int)hipGetLastError();
