@@ -111,6 +111,52 @@ def roofline_entry(summary, key, bound):
           "work_per_launch": s["avg_work"]}
 
 
+def decode_hbm_bytes(model, cfg, batch, ctx_lens, window):
+  """Algorithmic HBM bytes of ONE decode token-step for the whole batch:
+  every Griffin weight once (blocks + final norm + the tied embedding the
+  logits GEMM streams; the packed decode copies hold the same bytes), the
+  KV-cache reads of the local-attention blocks at the replayed context
+  lengths `ctx_lens` (mean), and the fp32 RG-LRU state read + write."""
+  wbytes = sum(p.numel() * p.element_size() for n, p in model.named_parameters()
+               if not n.startswith(("vis_encoder", "projector")))
+  kinds = [k.name for k in cfg.block_types[:cfg.num_layers]]
+  n_attn = kinds.count("ATTENTION")
+  n_rec = len(kinds) - n_attn
+  hd = cfg.width // cfg.num_heads
+  ctx = sum(min(c, window) for c in ctx_lens) / len(ctx_lens)
+  kv = n_attn * batch * ctx * 2 * hd * 2            # K and V, 1 kv head, bf16
+  state = n_rec * batch * cfg.lru_width * 4 * 2      # h read + write, fp32
+  return wbytes + kv + state
+
+
+def vit_attention_isolated(vis, batch, dev, reps=20):
+  """ViT attention alone (bench shapes, random qkv), HIP events around
+  `reps` back-to-back launches on the current stream: in the step the two
+  towers share the GPU, which stretches per-launch event windows."""
+  out = {}
+  for c in (vis.dino, vis.siglip):
+    n = vis.n_visual_tokens + c.num_prefix_tokens
+    qkv = torch.randn(batch * n, 3 * c.width, device=dev).to(torch.bfloat16)
+    ops.ops.vit_attention(qkv, batch, n, c.num_heads, c.head_dim)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+      ops.ops.vit_attention(qkv, batch, n, c.num_heads, c.head_dim)
+    e.record()
+    torch.cuda.synchronize()
+    us = s.elapsed_time(e) / reps * 1e3
+    flops = 4.0 * batch * c.num_heads * n * n * c.head_dim
+    tf = flops / (us * 1e-6) / 1e12
+    out[c.name] = {"kernel": f"vit_attn_kernel<hd{c.head_dim}>", "bound": "mfma",
+                   "achieved": round(tf, 2), "peak": MFMA_BF16_PEAK_TFS,
+                   "unit": "TFLOP/s", "frac": round(tf / MFMA_BF16_PEAK_TFS, 4),
+                   "avg_us": round(us, 2), "work_per_launch": flops,
+                   "shape": f"B={batch} N={n} H={c.num_heads} hd={c.head_dim}",
+                   "timing": f"isolated, {reps} launches after the timed region"}
+  return out
+
+
 def cpu_baseline(model, cfg, vis, tokens, images, decode_steps):
   """The oracle (reference op sequence, B = 1 like the reference) on host
   cores, on a bounded sample: 1 sample, full image + prompt prefill,
@@ -179,9 +225,15 @@ def main():
     t1 = time.perf_counter()
     ops.TIMER.enabled = False
   elapsed = D.max_over_ranks(t1 - t0)
+  decode_ms = []
   for ev in ev_list:
     prefill_ms.append(ev["prefill_start"].elapsed_time(ev["prefill_end"]))
+    if "decode_start" in ev:
+      decode_ms.append(ev["decode_start"].elapsed_time(ev["decode_end"])
+                       / ev["decode_steps"])
   ksum = ops.TIMER.summary() if not args.no_kernel_timing else {}
+  vit_iso = (vit_attention_isolated(vis, args.batch, dev)
+             if vis is not None and rank == 0 and not args.no_kernel_timing else None)
 
   tok_per_step = gb * (n_vis + args.prompt + args.decode)
   value = tok_per_step * args.steps / elapsed
@@ -192,8 +244,21 @@ def main():
 
   result = None
   if rank == 0:
-    gemm_keys = [k for k in ksum if k.startswith("gemm_tile_kernel")]
+    # dominant kernel: the single-kernel key with the most time in the step
+    gemm_keys = [k for k in ksum if k.startswith("gemm_big_kernel") and "+" not in k]
     dom = max(gemm_keys, key=lambda k: ksum[k]["total_ms"]) if gemm_keys else None
+    dec = None
+    if decode_ms:
+      # replayed steps 2..decode: context n_vis + prompt + i for step i
+      ctx = [n_vis + args.prompt + i for i in range(1, args.decode)]
+      nbytes = decode_hbm_bytes(model, cfg, args.batch, ctx,
+                                cfg.attention_window_size)
+      us = sum(decode_ms) / len(decode_ms) * 1e3
+      gbs = nbytes / (us * 1e-6) / 1e9
+      dec = {"kernel": "decode token-step (hipGraph, all kernels)",
+             "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+             "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+             "avg_us": round(us, 1), "work_per_launch": nbytes}
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -225,6 +290,10 @@ def main():
         "prefill_tokens_per_s": round(prefill_tps, 1),
         "roofline": roofline_entry(ksum, dom, "mfma") if dom else None,
         "roofline_scan": roofline_entry(ksum, "rnn_scan_kernel", "hbm"),
+        "roofline_decode": dec,
+        "roofline_vit_attention": vit_iso,
+        "roofline_by_kernel": {k: roofline_entry(ksum, k, "mfma") for k in sorted(ksum)
+                               if k.startswith(("gemm_big", "vit_attn", "flash_attn"))},
         "kernels": {k: {"launches": v["launches"],
                         "avg_us": round(v["avg_ms"] * 1e3, 2),
                         "total_ms_per_step": round(v["total_ms"] / args.steps, 3)}

@@ -107,7 +107,9 @@ class Sampler:
     """Prefill + decode for a left-padded [B, T] prompt batch (on device).
 
     `events`, if given, receives HIP events bracketing the prefill
-    ("prefill_start"/"prefill_end") on the current stream.
+    ("prefill_start"/"prefill_end") and the graph-replayed decode steps
+    ("decode_start"/"decode_end", with "decode_steps") on the decode
+    graph's stream.
     """
     dev = self.device
     b, t = tokens.shape
@@ -160,7 +162,7 @@ class Sampler:
                  and n_more > 1)
     if graphable:
       self._decode_graph(cur, pos, cache, buf, step, n_more,
-                         end_sampling_at_eos_token)
+                         end_sampling_at_eos_token, events)
     else:
       for i in range(n_more):
         nxt, logits, cache = model.next_token(cur[:, None], pos[:, None], cache,
@@ -194,7 +196,8 @@ class Sampler:
   def _all_done(self, buf: torch.Tensor) -> bool:
     return bool((buf == self.vocab.eos_id()).any(dim=1).all())
 
-  def _decode_graph(self, cur, pos, cache, buf, step, n_more, eos_stop):
+  def _decode_graph(self, cur, pos, cache, buf, step, n_more, eos_stop,
+                    events=None):
     """Replays a captured single-token decode step `n_more` times."""
     key = (cur.shape[0], cur.device)
     eng = self._graphs.get(key) if hasattr(self, "_graphs") else None
@@ -205,7 +208,7 @@ class Sampler:
                          cur.device)
       self._graphs[key] = eng
     eng.run(cache, cur, pos, buf, step, n_more,
-            (lambda b: self._all_done(b)) if eos_stop else None)
+            (lambda b: self._all_done(b)) if eos_stop else None, events)
 
   # ------------------------------------------------------------------- API
 
@@ -271,7 +274,7 @@ class _DecodeGraph:
     ops.ops.decode_advance_(nxt, self.buf, self.step, self.pos)
     self.cur.copy_(nxt)
 
-  def run(self, cache, cur, pos, buf, step, n_more, all_done=None):
+  def run(self, cache, cur, pos, buf, step, n_more, all_done=None, events=None):
     dev_stream = torch.cuda.current_stream(cur.device)
     for name, c in cache.items():
       for dst, src in zip(self.cache[name], c):
@@ -281,11 +284,18 @@ class _DecodeGraph:
     self.step.fill_(1)
     self.stream.wait_stream(dev_stream)
     with torch.cuda.stream(self.stream):
+      if events is not None:   # the replays alone (cache copies excluded)
+        events["decode_start"] = torch.cuda.Event(enable_timing=True)
+        events["decode_end"] = torch.cuda.Event(enable_timing=True)
+        events["decode_steps"] = n_more
+        events["decode_start"].record()
       for i in range(n_more):
         self.graph.replay()
         if all_done is not None and (i % 8 == 7) and all_done(
             self.buf[:, :buf.shape[1]]):
           break
+      if events is not None:
+        events["decode_end"].record()
     dev_stream.wait_stream(self.stream)
     steps = buf.shape[1]
     buf[:, 1:].copy_(self.buf[:, 1:steps])
