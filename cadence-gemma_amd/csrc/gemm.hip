@@ -522,6 +522,109 @@ __global__ __launch_bounds__(256, 2) void gemm_tile_kernel(
 typedef const void __attribute__((address_space(1)))* gptr_t;
 typedef void __attribute__((address_space(3)))* lptr_t;
 
+// 256 x 256 output tile of this workgroup: consecutive workgroups go to
+// consecutive XCDs, so each XCD takes a contiguous range of tiles, walked in
+// groups of 4 M-tiles (the W column panel is reused from that XCD's L2).
+CADENCE_DEV void big_tile_origin(int M, int N, int& m0, int& n0) {
+  constexpr int BM = 256, BN = 256, GM = 4;
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN, nt = ntm * ntn;
+  int t = blockIdx.x;
+  {
+    const int xcd = t & 7, q = nt >> 3, r = nt & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    t = base + (t >> 3);
+  }
+  const int grp = t / (GM * ntn), fm = grp * GM;
+  const int gs = min(ntm - fm, GM);
+  const int within = t % (GM * ntn);
+  const int tm = fm + within % gs, tn = within / gs;
+  m0 = tm * BM;
+  n0 = tn * BN;
+}
+
+// Epilogue of one wave's 128 x 64 accumulator block (rows mbase.., columns
+// nbase..; paired: 32 gate + 32 up packed columns).  Staged epilogues use
+// `st`, 16 KiB of idle operand LDS owned by this wave; the caller has
+// synchronised the workgroup and skipped padding column blocks.
+template <class Epi>
+CADENCE_DEV void big_epilogue(const Epi& epi, f32x4 (&acc)[8][4], u16* st, int mbase,
+                              int nbase, int lane, int M, int N, int g) {
+  constexpr int MR = 8, NR = 4;
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+  if constexpr (Epi::kStaged) {
+    // Stage the wave's first-rounding-point bf16 values in its own 16 KiB of
+    // the (now idle) operand LDS, [128 rows][64 cols] with a 16-B chunk XOR
+    // swizzle (paired: cols 0..31 gate half, 32..63 up half of the same 32
+    // logical columns), then a rolled loop finishes 8 columns of one row per
+    // lane and writes 16-B row segments.
+    constexpr int OC = Epi::kPaired ? 32 : 64;     // output columns per wave
+    constexpr int CPRW = OC / 8;                   // 16-B output chunks per row
+    auto sidx = [&](int r, int c) {
+      return r * 64 + (((c >> 3) ^ (r & 7)) << 3) + (c & 7);
+    };
+    float bcol[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      if constexpr (Epi::kPaired)
+        bcol[j] = epi.bias_at(j >= 2, nbase / 2 + (j & 1) * 16 + csub, g);
+      else
+        bcol[j] = epi.bias_at(false, min(nbase + j * 16 + csub, N - 1), g);
+    }
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          st[sidx(i * 16 + rsub + r, j * 16 + csub)] =
+              f2bf(epi.stage(acc[i][j][r], bcol[j]));
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    constexpr int RPI = 64 / CPRW;                 // rows per iteration
+    const int obase = Epi::kPaired ? nbase / 2 : nbase;
+    const int ch = lane % CPRW;
+#pragma unroll 2
+    for (int it = 0; it < 128 / RPI; ++it) {
+      const int lr = it * RPI + lane / CPRW;
+      const int row = mbase + lr;
+      const int col = obase + ch * 8;
+      const uint4 v = *reinterpret_cast<const uint4*>(&st[lr * 64 + ((ch ^ (lr & 7)) << 3)]);
+      if constexpr (Epi::kPaired) {
+        const uint4 u = *reinterpret_cast<const uint4*>(
+            &st[lr * 64 + (((ch + 4) ^ (lr & 7)) << 3)]);
+        if (row < M) epi.finish8p(row, col, v, u, g);
+      } else {
+        if (row < M && col < N) epi.finish8(row, col, v, g);
+      }
+    }
+  } else if constexpr (Epi::kTile) {
+    epi.template tile<MR>(acc, mbase, nbase, lane, M, N, g);
+  } else if constexpr (Epi::kPaired) {
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mbase + i * 16 + rsub + r;
+          if (row < M && nbase < N)
+            epi.apply2(row, nbase / 2 + j * 16 + csub, acc[i][j][r],
+                       acc[i][j + 2][r], g);
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mbase + i * 16 + rsub + r;
+          const int col = nbase + j * 16 + csub;
+          if (row < M && col < N) epi.apply(row, col, acc[i][j][r], g);
+        }
+  }
+}
+
 // 8-phase schedule (P8, K % 128 == 0).  The two LDS buffers (even / odd
 // K-tile) are each cut into four 16 KiB half-tiles by the wave sub-tile they
 // feed: A-h0 = rows {0..63, 128..191} (first 64 rows of each M-wave), A-h1 =
@@ -549,7 +652,7 @@ CADENCE_DEV void p8_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <class Epi, bool P8>
+template <class Epi, int P8>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
     int64_t ldw, int M, int N, int K, int64_t a_goff, int64_t w_goff,
@@ -562,19 +665,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
   A += g * a_goff;
   W += g * w_goff;
 
-  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN, nt = ntm * ntn;
-  int t = blockIdx.x;
-  {
-    const int xcd = t & 7, q = nt >> 3, r = nt & 7;
-    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-    t = base + (t >> 3);
-  }
-  constexpr int GM = 4;
-  const int grp = t / (GM * ntn), fm = grp * GM;
-  const int gs = min(ntm - fm, GM);
-  const int within = t % (GM * ntn);
-  const int tm = fm + within % gs, tn = within / gs;
-  const int m0 = tm * BM, n0 = tn * BN;
+  int m0, n0;
+  big_tile_origin(M, N, m0, n0);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -756,82 +848,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
   }
 
   const int mbase = m0 + wm * 128, nbase = n0 + wn * 64;
-  const int rsub = (lane >> 4) * 4, csub = lane & 15;
   if constexpr (Epi::kStaged) {
-    // Stage the wave's first-rounding-point bf16 values in its own 16 KiB of
-    // the (now idle) operand LDS, [128 rows][64 cols] with a 16-B chunk XOR
-    // swizzle (paired: cols 0..31 gate half, 32..63 up half of the same 32
-    // logical columns), then a rolled loop finishes 8 columns of one row per
-    // lane and writes 16-B row segments.
-    constexpr int OC = Epi::kPaired ? 32 : 64;     // output columns per wave
-    constexpr int CPRW = OC / 8;                   // 16-B output chunks per row
     __syncthreads();   // every wave is done reading the operand buffers
     if (nbase >= N) return;   // wave-uniform: this wave's columns are padding
-    u16* st = reinterpret_cast<u16*>(smem) + wave * (128 * 64);
-    auto sidx = [&](int r, int c) {
-      return r * 64 + (((c >> 3) ^ (r & 7)) << 3) + (c & 7);
-    };
-    float bcol[NR];
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      if constexpr (Epi::kPaired)
-        bcol[j] = epi.bias_at(j >= 2, nbase / 2 + (j & 1) * 16 + csub, g);
-      else
-        bcol[j] = epi.bias_at(false, min(nbase + j * 16 + csub, N - 1), g);
-    }
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          st[sidx(i * 16 + rsub + r, j * 16 + csub)] =
-              f2bf(epi.stage(acc[i][j][r], bcol[j]));
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    constexpr int RPI = 64 / CPRW;                 // rows per iteration
-    const int obase = Epi::kPaired ? nbase / 2 : nbase;
-    const int ch = lane % CPRW;
-#pragma unroll 2
-    for (int it = 0; it < 128 / RPI; ++it) {
-      const int lr = it * RPI + lane / CPRW;
-      const int row = mbase + lr;
-      const int col = obase + ch * 8;
-      const uint4 v = *reinterpret_cast<const uint4*>(&st[lr * 64 + ((ch ^ (lr & 7)) << 3)]);
-      if constexpr (Epi::kPaired) {
-        const uint4 u = *reinterpret_cast<const uint4*>(
-            &st[lr * 64 + (((ch + 4) ^ (lr & 7)) << 3)]);
-        if (row < M) epi.finish8p(row, col, v, u, g);
-      } else {
-        if (row < M && col < N) epi.finish8(row, col, v, g);
-      }
-    }
-  } else if constexpr (Epi::kTile) {
-    epi.template tile<MR>(acc, mbase, nbase, lane, M, N, g);
-  } else if constexpr (Epi::kPaired) {
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mbase + i * 16 + rsub + r;
-          if (row < M && nbase < N)
-            epi.apply2(row, nbase / 2 + j * 16 + csub, acc[i][j][r],
-                       acc[i][j + 2][r], g);
-        }
-  } else {
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mbase + i * 16 + rsub + r;
-          const int col = nbase + j * 16 + csub;
-          if (row < M && col < N) epi.apply(row, col, acc[i][j][r], g);
-        }
   }
+  big_epilogue(epi, acc, reinterpret_cast<u16*>(smem) + wave * (128 * 64), mbase,
+               nbase, lane, M, N, g);
 }
 
 // Weight-streaming decode GEMM (M <= 32).  One workgroup = NTW x 16 output
@@ -1298,6 +1320,8 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
     dim3 grid((unsigned)tiles, (unsigned)groups);
     // 8-phase pipeline when K splits into pairs of 64-deep tiles
     // (CADENCE_GEMM_P8=0 keeps the 2-buffer schedule for A/B runs)
+    // (an A/B of the guide's two-barrier phase -- reads, barrier, lgkmcnt(0),
+    // MFMAs, barrier -- ran 1-5 % slower on every prefill shape)
     static const bool p8_off = [] {
       const char* e = getenv("CADENCE_GEMM_P8");
       return e && e[0] == '0';
@@ -1305,10 +1329,10 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
     const bool p8 = !p8_off && K % (2 * BK) == 0;
     if constexpr (std::is_same_v<Epi, EpiLinear>) {
 #define CADENCE_BIG_ACT(ACT_)                                                          \
-  if (p8) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, true>), grid, dim3(512), \
-                             0, st, A, lda, W, ldw, (int)M, (int)N, (int)K, a_goff,     \
-                             w_goff, EpiLinearA<ACT_>{epi});                            \
-  else hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, false>), grid, dim3(512),  \
+  if (p8) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 1>), grid,         \
+                             dim3(512), 0, st, A, lda, W, ldw, (int)M, (int)N, (int)K,  \
+                             a_goff, w_goff, EpiLinearA<ACT_>{epi});                    \
+  else hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 0>), grid, dim3(512),      \
                           0, st, A, lda, W, ldw, (int)M, (int)N, (int)K, a_goff,        \
                           w_goff, EpiLinearA<ACT_>{epi})
       switch (epi.act) {
@@ -1320,10 +1344,10 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
       }
 #undef CADENCE_BIG_ACT
     } else if (p8) {
-      hipLaunchKernelGGL((gemm_big_kernel<Epi, true>), grid, dim3(512), 0, st, A, lda, W,
+      hipLaunchKernelGGL((gemm_big_kernel<Epi, 1>), grid, dim3(512), 0, st, A, lda, W,
                          ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
     } else {
-      hipLaunchKernelGGL((gemm_big_kernel<Epi, false>), grid, dim3(512), 0, st, A, lda, W,
+      hipLaunchKernelGGL((gemm_big_kernel<Epi, 0>), grid, dim3(512), 0, st, A, lda, W,
                          ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
     }
     return (int)hipGetLastError();

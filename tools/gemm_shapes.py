@@ -41,6 +41,11 @@ def main():
     us = timeit(lambda: ops.linear(a, w, out=out))
     print(f"{tag:6s} M={M:6d} N={N:6d} K={K:5d} {us:8.1f} us "
           f"{2*M*N*K/us/1e6:7.1f} TF/s  out {M*N*2/us/1e3:6.0f} GB/s", flush=True)
+    if os.environ.get("VS_TORCH") == "1":   # hipBLASLt through torch.mm
+      wt = w.t()
+      us = timeit(lambda: torch.mm(a, wt, out=out))
+      print(f"torch  M={M:6d} N={N:6d} K={K:5d} {us:8.1f} us "
+            f"{2*M*N*K/us/1e6:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
