@@ -194,18 +194,19 @@ class RecurrentBlock(nn.Module):
             inplace_state: bool = False, norm=None):
     e = self.lru_width
     w, bias = self.yx_weight()
-    yx = ops.linear(xn2d, w, bias)                       # [M, 2E]: y | x
-    y_br, x_br = yx[:, :e], yx[:, e:]
     if (inplace_state and return_cache and cache is not None and t == 1 and
-        cache.conv1d_state.is_contiguous() and
+        b <= 32 and cache.conv1d_state.is_contiguous() and
         cache.conv1d_state.dtype == xn2d.dtype):
-      # decode: conv / RG-LRU states are advanced in place by the kernels
-      conv_out = ops.ops.conv1d_step_(x_br, self.conv_1d.w, self.conv_1d.b,
-                                      cache.conv1d_state)
-      gated = self.rg_lru.step_(conv_out, pos.view(-1), cache.rg_lru_state,
-                                y_br, packed_out=True)
+      # decode: the y|x projection runs the x branch's Conv1D step in its
+      # epilogue; conv / RG-LRU states are advanced in place by the kernels
+      yc = ops.linear_conv1d_(xn2d, w, bias, self.conv_1d.w, self.conv_1d.b,
+                              cache.conv1d_state)       # [M, 2E]: y | conv(x)
+      gated = self.rg_lru.step_(yc[:, e:], pos.view(-1), cache.rg_lru_state,
+                                yc[:, :e], packed_out=True)
       out, hn = _out_proj(gated, self.linear_out, resid2d, norm)
       return out, hn, cache
+    yx = ops.linear(xn2d, w, bias)                       # [M, 2E]: y | x
+    y_br, x_br = yx[:, :e], yx[:, e:]
     conv_out, conv_state = self.conv_1d.apply2d(
         x_br, pos, None if cache is None else cache.conv1d_state, b, t)
     a, nx = self.rg_lru.gates(conv_out, pos.view(-1))

@@ -260,6 +260,35 @@ def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off,
   TIMER.stop(ev, f"gemm_big_kernel<EpiLinearA<{act}>>", 2.0 * M * N * K, a)
 
 
+@_reg("gemm_linear_conv1d_(Tensor a, Tensor w, Tensor? bias, Tensor conv_w, "
+      "Tensor conv_b, Tensor(a!) conv_state, bool w_packed=False, "
+      "int a_rows=-1) -> Tensor")
+def _gemm_linear_conv1d(a, w, bias, conv_w, conv_b, conv_state, w_packed=False,
+                        a_rows=-1):
+  """Decode y|x projection fused with the x branch's Conv1D step: returns
+  [M, 2E] = (y, conv1d_step(x)); `conv_state` [M, TW-1, E] advances in place."""
+  ldw = _wld(w, w_packed, "w")
+  N, K = w.shape[0], w.shape[1]
+  if a_rows >= 0:
+    lda, M = 0, a_rows
+    _need(a.numel() == K * 16 * (-(-M // 16)), "a: packed rows size")
+  else:
+    lda = _mat(a, "a")
+    M, K = a.shape
+  TW, E = conv_w.shape
+  _need(N == 2 * E and conv_b.numel() == E, "conv width vs projection width")
+  _need(conv_state.is_contiguous() and conv_state.dtype == _BF16 and
+        tuple(conv_state.shape) == (M, TW - 1, E), "conv state")
+  if bias is not None:
+    _need(bias.numel() == N and bias.dtype == _BF16, "bias shape/dtype")
+  out = torch.empty(M, N, dtype=_BF16, device=a.device)
+  _lib.check(_lib.load().cadence_gemm_linear_conv1d(
+      _p(a), lda, _p(w), ldw, _p(bias), _p(out), N, M, N, K, E,
+      _p(conv_w.contiguous()), _p(conv_b.contiguous()), _p(conv_state), TW, _s(a)),
+      "gemm_linear_conv1d")
+  return out
+
+
 @_reg("gemm_linear_rmsnorm(Tensor a, Tensor w, Tensor? bias, Tensor? resid, "
       "Tensor scale, float eps, bool w_packed=False, int a_rows=-1, "
       "bool norm_packed=False) -> (Tensor, Tensor)")
@@ -750,6 +779,17 @@ def linear(x2d, w, bias=None, act=0, resid=None, out=None,
   else:
     ops.gemm_linear_(a, w, bias, resid, out, act, div, mul, off, False, ar)
   return out
+
+
+def linear_conv1d_(x2d, w, bias, conv_w, conv_b, conv_state):
+  """Decode recurrent-block input projection: (y, conv1d_step(x)) as one
+  [M, 2E] tensor, the conv state advanced in place."""
+  M = x2d.shape[0]
+  a, ar = _a(x2d)
+  wd = decode_weight(w)
+  if wd is not None:
+    return ops.gemm_linear_conv1d_(a, wd, bias, conv_w, conv_b, conv_state, True, ar)
+  return ops.gemm_linear_conv1d_(a, w, bias, conv_w, conv_b, conv_state, False, ar)
 
 
 def linear_rmsnorm(x2d, w, bias, resid, norm, packed_out=None):

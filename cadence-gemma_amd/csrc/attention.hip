@@ -312,27 +312,43 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
   const int tps = (ntot + NS - 1) / NS;
   const int tb = min(ntot, split * tps), te = min(ntot, tb + tps);
   (void)nslots;
+  // K / V chunks of a tile in registers; tile ti+1 is fetched while tile ti
+  // is computed (one memory latency per split instead of one per tile)
+  constexpr int CH = KT * CPR / 256;
+  uint4 kreg[CH], vreg[CH];
+  auto fetch = [&](int ti) {
+    const int k0 = (ti < ring_tiles ? ti : last_tile) * KT;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = tid + i * 256;
+      const int kr = c / CPR, d = (c % CPR) * 8;
+      const int slot = k0 + kr;
+      kreg[i] = vreg[i] = make_uint4(0, 0, 0, 0);
+      if (slot < a.W) {
+        kreg[i] = ld16(ckb + (int64_t)slot * a.hd + d);
+        vreg[i] = ld16(cvb + (int64_t)slot * a.hd + d);
+      } else if (slot == a.W) {
+        kreg[i] = ld16(a.k_new + (int64_t)b * a.new_rs + d);
+        vreg[i] = ld16(a.v_new + (int64_t)b * a.new_rs + d);
+      }
+    }
+  };
+  if (tb < te) fetch(tb);
   for (int ti = tb; ti < te; ++ti) {
     const int k0 = (ti < ring_tiles ? ti : last_tile) * KT;
     __syncthreads();
-    for (int c = tid; c < KT * CPR; c += 256) {
-      const int kr = c / CPR, ch = c % CPR;
-      const int slot = k0 + kr;
-      const int d = ch * 8;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-      if (slot < a.W) {
-        kv = ld16(ckb + (int64_t)slot * a.hd + d);
-        vv = ld16(cvb + (int64_t)slot * a.hd + d);
-      } else if (slot == a.W) {
-        kv = ld16(a.k_new + (int64_t)b * a.new_rs + d);
-        vv = ld16(a.v_new + (int64_t)b * a.new_rs + d);
-      }
-      ks_[kr * CPR + swz<CPR>(ch, kr)] = kv;
-      const u16* vs = reinterpret_cast<const u16*>(&vv);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) vt[(d + i) * KT + kr] = vs[i];
+    for (int i = 0; i < CH; ++i) {
+      const int c = tid + i * 256;
+      const int kr = c / CPR, ch = c % CPR;
+      const int d = ch * 8;
+      ks_[kr * CPR + swz<CPR>(ch, kr)] = kreg[i];
+      const u16* vs = reinterpret_cast<const u16*>(&vreg[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vt[(d + j) * KT + kr] = vs[j];
     }
     __syncthreads();
+    if (ti + 1 < te) fetch(ti + 1);
     f32x4 s[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int jn = 0; jn < 2; ++jn) {
@@ -455,28 +471,47 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
     if (ticket != NS - 1) return;
     const int nsp = (ntot + tps - 1) / tps;     // splits that held tiles
     const float* pb = a.parts + (int64_t)b * NS * PS;
-    for (int q = tid * 4; q < 16 * HD; q += 1024) {
+    // every load of the combine is issued before the first use (fixed trip
+    // counts, splits >= nsp predicated off): one memory round trip instead
+    // of one per (row chunk, split)
+    constexpr int QI = 16 * HD / 1024;          // row chunks per thread
+    float ms[QI][kDecodeSplits], ls[QI][kDecodeSplits];
+    uint64_t w0[QI][kDecodeSplits], w1[QI][kDecodeSplits];
+#pragma unroll
+    for (int it = 0; it < QI; ++it) {
+      const int q = tid * 4 + it * 1024;
+      const int hrow = q / HD;
+#pragma unroll
+      for (int sp = 0; sp < kDecodeSplits; ++sp) {
+        const bool on = sp < nsp && hrow < a.H;
+        const float* base = pb + (on ? sp : 0) * PS;
+        ms[it][sp] = __hip_atomic_load(base + hrow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ls[it][sp] = __hip_atomic_load(base + 16 + hrow, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(base + 32 + q);
+        w0[it][sp] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        w1[it][sp] = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < QI; ++it) {
+      const int q = tid * 4 + it * 1024;
       const int hrow = q / HD;
       if (hrow >= a.H) continue;
       float mx = -INFINITY;
-      for (int sp = 0; sp < nsp; ++sp)
-        mx = fmaxf(mx, __hip_atomic_load(pb + sp * PS + hrow, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+      for (int sp = 0; sp < kDecodeSplits; ++sp)
+        if (sp < nsp) mx = fmaxf(mx, ms[it][sp]);
       float l = 0.0f, acc[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int sp = 0; sp < nsp; ++sp) {
-        const float ms = __hip_atomic_load(pb + sp * PS + hrow, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-        const float ls = __hip_atomic_load(pb + sp * PS + 16 + hrow, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-        const float wgt = (ms == -INFINITY) ? 0.0f : expf(ms - mx);
-        l += ls * wgt;
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(pb + sp * PS + 32 + q);
-        const uint64_t w0 = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t w1 = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc[0] += __uint_as_float((uint32_t)w0) * wgt;
-        acc[1] += __uint_as_float((uint32_t)(w0 >> 32)) * wgt;
-        acc[2] += __uint_as_float((uint32_t)w1) * wgt;
-        acc[3] += __uint_as_float((uint32_t)(w1 >> 32)) * wgt;
+#pragma unroll
+      for (int sp = 0; sp < kDecodeSplits; ++sp) {
+        if (sp >= nsp) continue;
+        const float wgt = (ms[it][sp] == -INFINITY) ? 0.0f : expf(ms[it][sp] - mx);
+        l += ls[it][sp] * wgt;
+        acc[0] += __uint_as_float((uint32_t)w0[it][sp]) * wgt;
+        acc[1] += __uint_as_float((uint32_t)(w0[it][sp] >> 32)) * wgt;
+        acc[2] += __uint_as_float((uint32_t)w1[it][sp]) * wgt;
+        acc[3] += __uint_as_float((uint32_t)(w1[it][sp] >> 32)) * wgt;
       }
       const float inv = l > 0.0f ? 1.0f / l : 0.0f;
       u16* dst = a.o + xoff(b, q, a.ldo, a.omt);

@@ -71,6 +71,7 @@ CADENCE_DEV float softcap(float l, float c) {
 //    cache (an unrolled gate chain made the kernel 160 KB and cost ~25 us of
 //    instruction fetch per tile).
 struct EpiLinear {
+  struct Pref {};
   static constexpr bool kPaired = false;
   static constexpr bool kStaged = true;
   static constexpr bool kTile = false;
@@ -142,6 +143,66 @@ struct EpiLinearA : EpiLinear {
       return r;
     });
   }
+};
+
+// Decode yx projection fused with the Conv1D decode step of the x branch
+// (stream engine only, M <= 32 rows = sequences): columns >= conv_lo are the
+// x branch; their rounded linear output x_t enters the depthwise causal
+// conv [state rows (TW-1) | x_t] (layers.py:478-483, same products, sums and
+// roundings as conv1d_decode_kernel), the conv output replaces x_t in `out`
+// and the state rows shift in place.  Each (row, channel) is owned by one
+// thread; its conv operands are loaded at kernel start (kPrefetch) so they
+// land while the weight stream is in flight.
+template <int TW>
+struct EpiLinearConv : EpiLinear {
+  static constexpr bool kPrefetch = true;
+  const u16* cw;         // [TW][E] conv weight
+  const u16* cb;         // [E] conv bias
+  u16* state;            // [M][TW-1][E], advanced in place
+  int conv_lo, E;
+  struct Pref { u16 w[TW], s[TW > 1 ? TW - 1 : 1], b; };
+  CADENCE_DEV Pref prefetch(int64_t m, int n) const {
+    Pref p{};
+    if (n >= conv_lo) {
+      const int c = n - conv_lo;
+      const u16* srow = state + m * (int64_t)(TW - 1) * E + c;
+#pragma unroll
+      for (int t = 0; t < TW; ++t) p.w[t] = cw[(int64_t)t * E + c];
+#pragma unroll
+      for (int r = 0; r < TW - 1; ++r) p.s[r] = srow[(int64_t)r * E];
+      p.b = cb[c];
+    }
+    return p;
+  }
+  CADENCE_DEV void apply_pf(int64_t m, int n, float v, int g, const Pref& p) const {
+    const float x = value(m, n, v, g);          // act 0: bias + one rounding
+    if (n < conv_lo) {
+      out[m * ldo + n] = f2bf(x);
+      return;
+    }
+    // [state rows | x_t] . w, newest first: conv1d_decode_kernel's order
+    float acc = bmul(x, bf2f(p.w[TW - 1]));
+#pragma unroll
+    for (int s = 1; s < TW; ++s)
+      acc = badd(acc, bmul(bf2f(p.s[TW - 1 - s]), bf2f(p.w[TW - 1 - s])));
+    acc = badd(acc, bf2f(p.b));
+    out[m * ldo + n] = f2bf(acc);
+    u16* srow = state + m * (int64_t)(TW - 1) * E + (n - conv_lo);
+#pragma unroll
+    for (int r = 0; r + 1 < TW - 1; ++r) srow[(int64_t)r * E] = p.s[r + 1];
+    if constexpr (TW > 1) srow[(int64_t)(TW - 2) * E] = f2bf(x);
+  }
+  CADENCE_DEV void apply(int64_t m, int n, float v, int g) const {
+    apply_pf(m, n, v, g, prefetch(m, n));
+  }
+};
+
+// Epilogues that load per-element operands at kernel start (kPrefetch).
+template <class E, class = void>
+struct EpiPrefetch { static constexpr bool value = false; };
+template <class E>
+struct EpiPrefetch<E, std::void_t<decltype(E::kPrefetch)>> {
+  static constexpr bool value = E::kPrefetch;
 };
 
 struct EpiGatedGelu {
@@ -887,6 +948,18 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
 #pragma unroll
     for (int t = 0; t < NTW; ++t) col[t] = (blockIdx.x * NTW + t) * 16;
   }
+  // prefetching epilogues: this thread's epilogue elements are row tid / 16,
+  // columns col[j] + tid % 16 (the epilogue loop below runs once per thread)
+  constexpr bool kPf = EpiPrefetch<Epi>::value;
+  [[maybe_unused]] typename std::conditional<kPf, Epi, EpiLinear>::type::Pref pf[NREP];
+  if constexpr (kPf) {
+    static_assert(!Epi::kPaired && MS * 16 <= 512, "one epilogue element per thread");
+    if ((int)threadIdx.x < MS * 16 && (int)(threadIdx.x >> 4) < M && !parts) {
+#pragma unroll
+      for (int j = 0; j < NREP; ++j)
+        pf[j] = epi.prefetch(threadIdx.x >> 4, col[j] + (threadIdx.x & 15));
+    }
+  }
   const int koff = 8 * (lane >> 4);
   const int kbeg = blockIdx.y * klen;
   const int kend = min(K, kbeg + klen);
@@ -959,6 +1032,9 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
     } else if constexpr (Epi::kPaired) {
       const int grp = blockIdx.x >> 1, half = blockIdx.x & 1;
       epi.apply2(m, grp * 32 + half * 16 + c, v[0], v[NREP - 1], g);
+    } else if constexpr (kPf) {
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) epi.apply_pf(m, col[j] + c, v[j], g, pf[j]);
     } else {
 #pragma unroll
       for (int j = 0; j < NREP; ++j) epi.apply(m, col[j] + c, v[j], g);
@@ -1428,6 +1504,44 @@ int cadence_gemm_linear(const void* A, int64_t lda, const void* W, int64_t ldw,
   return launch_gemm(static_cast<const u16*>(A), lda, static_cast<const u16*>(W),
                      ldw, M, N, K, 1, 0, 0, epi, workspace, ws_bytes,
                      static_cast<hipStream_t>(stream));
+}
+
+int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
+                               int64_t ldw, const void* bias, void* out,
+                               int64_t ldo, int64_t M, int64_t N, int64_t K,
+                               int64_t conv_lo, const void* conv_w,
+                               const void* conv_b, void* conv_state,
+                               int64_t temporal_width, void* stream) {
+  if (M <= 0) return 0;
+  const int64_t E = N - conv_lo;
+  int ksw = 0, ss = 0;
+  if (M > 32 || N % 64 || K % 32 || ldo < N || conv_lo < 0 || E <= 0 ||
+      temporal_width < 1 || temporal_width > 4 || !conv_w || !conv_b ||
+      (temporal_width > 1 && !conv_state) || (ldw != 0 && ldw < K) ||
+      (lda != 0 && lda < K) || !stream_plan(M, K, &ksw, &ss) || ss != 1)
+    return (int)hipErrorInvalidValue;
+  const EpiLinear base{static_cast<u16*>(out), ldo, static_cast<const u16*>(bias),
+                       nullptr, 0, 0, RowMap{M, 0, 0}, 0.0f};
+  auto run = [&](auto tw_tag) {
+    constexpr int TW = decltype(tw_tag)::value;
+    EpiLinearConv<TW> epi{};
+    static_cast<EpiLinear&>(epi) = base;
+    epi.cw = static_cast<const u16*>(conv_w);
+    epi.cb = static_cast<const u16*>(conv_b);
+    epi.state = static_cast<u16*>(conv_state);
+    epi.conv_lo = (int)conv_lo;
+    epi.E = (int)E;
+    launch_stream(static_cast<const u16*>(A), lda, static_cast<const u16*>(W), ldw, M,
+                  N, K, 1, 0, 0, epi, ksw, 1, nullptr, ldw == 0 ? 1 : 0,
+                  static_cast<hipStream_t>(stream));
+  };
+  switch (temporal_width) {   // Griffin uses 4; 1-3 for API parity
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    case 3: run(std::integral_constant<int, 3>{}); break;
+    default: run(std::integral_constant<int, 4>{}); break;
+  }
+  return (int)hipGetLastError();
 }
 
 int64_t cadence_gemm_rmsnorm_workspace_bytes(int64_t M, int64_t N, int64_t K) {

@@ -22,26 +22,36 @@
 
 namespace {
 
-template <int CPR>
+// K image: KW stored 16-B chunks per key row, XOR-swizzled so that the
+// 16-lane ds_read_b128 groups of a k-step are conflict-free (checked
+// exhaustively for both row strides): 8 chunks (128-B rows): ch ^ (row & 7);
+// 10 chunks (160-B rows): chunks 0-7 ^ ((row >> 2) & 7), the pair 8-9 ^ (row & 1).
+template <int KW>
 CADENCE_DEV int kswz(int ch, int row) {
-  return (CPR % 8 == 0) ? (ch ^ (row & 7)) : (ch ^ (row & 3));
+  if constexpr (KW == 8) return ch ^ (row & 7);
+  return ch < 8 ? (ch ^ ((row >> 2) & 7)) : (8 + ((ch - 8) ^ (row & 1)));
 }
 
 // HDK: head dim padded to a multiple of 32 (QK^T k-steps); HDV: padded to 16
 // (O^T row tiles); NPMAX: LDS capacity in keys (multiple of 32); NW waves;
-// QT query tiles per wave pass.
-template <int HDK, int HDV, int NPMAX, int NW, int QT>
+// QT query tiles per wave pass.  Only what the head dim needs is stored:
+// KW = ceil(hd / 8) chunks of each K row (a k-step chunk past KW re-reads
+// chunk KW - 2 or KW - 1 of the same row: finite, and its Q fragment is
+// zero) and VR = hd rows of V^T (O^T rows >= hd read row VR - 1 and are
+// discarded) -- for hd 72 that is 79 KB, two workgroups per CU.
+template <int HDK, int HDV, int NPMAX, int NW, int QT, int KW = HDK / 8, int VR = HDV>
 __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
     const u16* __restrict__ qkv, u16* __restrict__ out, int N, int H, int hd,
     float scale_log2, int dbg) {
-  constexpr int CPR = HDK / 8;        // 16-B chunks per K row
+  constexpr int CPR = KW;             // stored 16-B chunks per K row
   constexpr int KS = HDK / 32;
   constexpr int NDT = HDV / 16;
-  constexpr int VCH = HDV / 8;
+  constexpr int VCH = VR / 8;         // stored V^T row groups of 8 dims
   constexpr int VTS = NPMAX + 8;      // V^T row stride (elements): 16-B pad
   constexpr int KIMG = NPMAX * CPR;   // uint4 of the K image
+  static_assert(KW % 2 == 0 && KW >= 8 && KW * 8 <= HDK && VR % 8 == 0, "layout");
   // one LDS array (K image, then V^T)
-  __shared__ __attribute__((aligned(16))) uint4 smem[KIMG + (HDV * VTS) / 8];
+  __shared__ __attribute__((aligned(16))) uint4 smem[KIMG + (VR * VTS) / 8];
   uint4* kimg = smem;
   u16* vt = reinterpret_cast<u16*>(smem + KIMG);
 
@@ -143,7 +153,9 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
         const int kr = c0 + 16 * t + c16;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          const bf16x8 kf = __builtin_bit_cast(bf16x8, kimg[kr * CPR + kswz<CPR>(ks * 4 + g, kr)]);
+          const int lc = ks * 4 + g;
+          const int ch = lc < CPR ? lc : lc - 2;   // past the stored chunks
+          const bf16x8 kf = __builtin_bit_cast(bf16x8, kimg[kr * CPR + kswz<CPR>(ch, kr)]);
 #pragma unroll
           for (int u = 0; u < QT; ++u)
             s[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[u][ks], s[u][t], 0, 0, 0);
@@ -204,7 +216,8 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
         if (kk == 1 && two) continue;
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
-          const u16* vr = vt + (dt * 16 + c16) * VTS + c0 + 32 * kk + 4 * g;
+          const int vrow = min(dt * 16 + c16, VR - 1);   // rows >= VR: discarded dims
+          const u16* vr = vt + vrow * VTS + c0 + 32 * kk + 4 * g;
           const uint2 lo = *reinterpret_cast<const uint2*>(vr);
           const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
           const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
@@ -263,23 +276,24 @@ __attribute__((visibility("hidden"))) int vit_attention_lds_launch(
   const dim3 grid((unsigned)H, (unsigned)B);
   const u16* in = static_cast<const u16*>(qkv);
   u16* o = static_cast<u16*>(out);
-#define VA(HDK_, HDV_, NP_, NW_, QT_)                                                \
-  hipLaunchKernelGGL((vit_attn_kernel<HDK_, HDV_, NP_, NW_, QT_>), grid, dim3(NW_ * 64), \
-                     0, st, in, o, (int)N, (int)H, (int)hd, sl2, dbg)
-#define VSEL(HDK_, HDV_, NP_, DEF_NW, DEF_QT)                                        \
-  switch (cfg ? cfg : DEF_NW * 10 + DEF_QT) {                                        \
-    case 41: VA(HDK_, HDV_, NP_, 4, 1); break;                                       \
-    case 42: VA(HDK_, HDV_, NP_, 4, 2); break;                                       \
-    case 81: VA(HDK_, HDV_, NP_, 8, 1); break;                                       \
-    case 82: VA(HDK_, HDV_, NP_, 8, 2); break;                                       \
-    default: return -1;                                                              \
+#define VA(HDK_, HDV_, NP_, NW_, QT_, KW_, VR_)                                       \
+  hipLaunchKernelGGL((vit_attn_kernel<HDK_, HDV_, NP_, NW_, QT_, KW_, VR_>), grid,       \
+                     dim3(NW_ * 64), 0, st, in, o, (int)N, (int)H, (int)hd, sl2, dbg)
+#define VSEL(HDK_, HDV_, NP_, KW_, VR_, DEF)                                          \
+  switch (cfg ? cfg : DEF) {                                                          \
+    case 81: VA(HDK_, HDV_, NP_, 8, 1, KW_, VR_); break;                              \
+    case 82: VA(HDK_, HDV_, NP_, 8, 2, KW_, VR_); break;                              \
+    default: return -1;                                                               \
   }
+  // 8 waves x 1 query tile (DINO's 17 tiles on 9 waves measured 10 % slower:
+  // 18 waves per CU do not split evenly over the 4 SIMDs)
+  const int def = 81;
   if (hd == 64 && N <= 288) {
-    VSEL(64, 64, 288, 8, 1)
+    VSEL(64, 64, 288, 8, 64, def)
   } else if (hd == 72 && N <= 256) {
-    VSEL(96, 80, 256, 8, 1)
+    VSEL(96, 80, 256, 10, 72, def)
   } else if (hd == 72 && N <= 288) {
-    VSEL(96, 80, 288, 8, 1)
+    VSEL(96, 80, 288, 10, 72, def)
   } else {
     return -1;
   }

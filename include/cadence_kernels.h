@@ -80,6 +80,23 @@ int cadence_gemm_linear(const void* A, int64_t lda, const void* W, int64_t ldw,
                         int64_t row_off, void* workspace, int64_t ws_bytes,
                         void* stream);
 
+/* Decode (M <= 32 sequences, one token each) projection of the recurrent
+ * block's two branches fused with the Conv1D decode step of the x branch
+ * (replaces cadence_gemm_linear + cadence_conv1d with a cache, L == 1;
+ * reference modules.py:340-352 linear_y / linear_x, layers.py:478-483):
+ *   yx = A . W^T + bias                    (W = [linear_y; linear_x], N = 2E)
+ *   out[:, :conv_lo]  = yx[:, :conv_lo]    (the y branch, as is)
+ *   out[:, conv_lo:]  = conv1d_step(yx[:, conv_lo:]; conv_w [TW][E], conv_b,
+ *                                   conv_state [M][TW-1][E], shifted in place)
+ * W may be fragment-packed (ldw == 0) and A packed rows (lda == 0).  K must
+ * fit one split of the weight-streaming engine (K <= 2560); TW <= 4. */
+int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
+                               int64_t ldw, const void* bias, void* out,
+                               int64_t ldo, int64_t M, int64_t N, int64_t K,
+                               int64_t conv_lo, const void* conv_w,
+                               const void* conv_b, void* conv_state,
+                               int64_t temporal_width, void* stream);
+
 /* Residual GEMM that feeds an RMSNorm (the temporal-block output projection
  * and ffw_down, each followed by the next norm; modules.py:908-913):
  *   out = A . W^T + bias + resid          (as cadence_gemm_linear, act 0)
