@@ -583,11 +583,12 @@ __global__ __launch_bounds__(256, 2) void gemm_tile_kernel(
 typedef const void __attribute__((address_space(1)))* gptr_t;
 typedef void __attribute__((address_space(3)))* lptr_t;
 
-// 256 x 256 output tile of this workgroup: consecutive workgroups go to
+// BM x 256 output tile of this workgroup: consecutive workgroups go to
 // consecutive XCDs, so each XCD takes a contiguous range of tiles, walked in
 // groups of 4 M-tiles (the W column panel is reused from that XCD's L2).
+template <int BM>
 CADENCE_DEV void big_tile_origin(int M, int N, int& m0, int& n0) {
-  constexpr int BM = 256, BN = 256, GM = 4;
+  constexpr int BN = 256, GM = 4;
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN, nt = ntm * ntn;
   int t = blockIdx.x;
   {
@@ -603,14 +604,14 @@ CADENCE_DEV void big_tile_origin(int M, int N, int& m0, int& n0) {
   n0 = tn * BN;
 }
 
-// Epilogue of one wave's 128 x 64 accumulator block (rows mbase.., columns
-// nbase..; paired: 32 gate + 32 up packed columns).  Staged epilogues use
-// `st`, 16 KiB of idle operand LDS owned by this wave; the caller has
-// synchronised the workgroup and skipped padding column blocks.
-template <class Epi>
-CADENCE_DEV void big_epilogue(const Epi& epi, f32x4 (&acc)[8][4], u16* st, int mbase,
+// Epilogue of one wave's (16 MR) x 64 accumulator block (rows mbase..,
+// columns nbase..; paired: 32 gate + 32 up packed columns).  Staged
+// epilogues use `st`, 16 KiB of idle operand LDS owned by this wave; the
+// caller has synchronised the workgroup and skipped padding column blocks.
+template <class Epi, int MR>
+CADENCE_DEV void big_epilogue(const Epi& epi, f32x4 (&acc)[MR][4], u16* st, int mbase,
                               int nbase, int lane, int M, int N, int g) {
-  constexpr int MR = 8, NR = 4;
+  constexpr int NR = 4;
   const int rsub = (lane >> 4) * 4, csub = lane & 15;
   if constexpr (Epi::kStaged) {
     // Stage the wave's first-rounding-point bf16 values in its own 16 KiB of
@@ -645,7 +646,7 @@ CADENCE_DEV void big_epilogue(const Epi& epi, f32x4 (&acc)[8][4], u16* st, int m
     const int obase = Epi::kPaired ? nbase / 2 : nbase;
     const int ch = lane % CPRW;
 #pragma unroll 2
-    for (int it = 0; it < 128 / RPI; ++it) {
+    for (int it = 0; it < MR * 16 / RPI; ++it) {
       const int lr = it * RPI + lane / CPRW;
       const int row = mbase + lr;
       const int col = obase + ch * 8;
@@ -713,13 +714,17 @@ CADENCE_DEV void p8_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <class Epi, int P8>
+// MR = 7 (BM = 224, P8 only): the second m-half of each wave holds 3
+// fragments (48 rows); its half-tile DMA re-loads the last of those rows
+// into the unused 16 rows, so every wave issues the same DMA count.
+template <class Epi, int P8, int MR = 8>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
     int64_t ldw, int M, int N, int K, int64_t a_goff, int64_t w_goff,
     Epi epi) {
-  constexpr int BM = 256, BN = 256, MR = 8, NR = 4;
-  constexpr int ROWS = BM + BN;               // LDS rows per buffer (128 B)
+  constexpr int BM = 32 * MR, BN = 256, NR = 4;
+  static_assert(MR == 8 || (P8 && MR >= 5 && MR < 8), "BM < 256 needs the 8-phase schedule");
+  constexpr int ROWS = 256 + BN;              // LDS rows per buffer (128 B)
   __shared__ __attribute__((aligned(16))) uint4 smem[2 * ROWS * 8];
 
   const int g = blockIdx.y;
@@ -727,7 +732,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
   W += g * w_goff;
 
   int m0, n0;
-  big_tile_origin(M, N, m0, n0);
+  big_tile_origin<BM>(M, N, m0, n0);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -751,7 +756,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
 #pragma unroll
       for (int pc = 0; pc < 2; ++pc) {
         const int r = (2 * wave + pc) * 8 + (lane >> 3);   // half-tile row
-        const int gm = min(m0 + (r >> 6) * 128 + h * 64 + (r & 63), M - 1);
+        const int rr = h ? min(r & 63, MR * 16 - 65) : (r & 63);
+        const int gm = min(m0 + (r >> 6) * (MR * 16) + h * 64 + rr, M - 1);
         const int gn = min(n0 + (r >> 5) * 64 + h * 32 + (r & 31), N - 1);
         sa[h][pc] = A + (int64_t)gm * lda + src_chunk * 8;
         sb[h][pc] = W + (int64_t)gn * ldw + src_chunk * 8;
@@ -766,7 +772,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
     auto readA = [&](int buf, int mh) {
       const uint4* base = &smem[(buf * 4 + mh) * HT];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < (mh ? MR - 4 : 4); ++i)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           af[i][ks] = __builtin_bit_cast(
@@ -786,7 +792,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
     auto mma = [&](int mh, int nh, const bf16x8 (&bf)[2][2]) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < (mh ? MR - 4 : 4); ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -908,12 +914,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
   }
   }
 
-  const int mbase = m0 + wm * 128, nbase = n0 + wn * 64;
+  const int mbase = m0 + wm * (MR * 16), nbase = n0 + wn * 64;
   if constexpr (Epi::kStaged) {
     __syncthreads();   // every wave is done reading the operand buffers
     if (nbase >= N) return;   // wave-uniform: this wave's columns are padding
   }
-  big_epilogue(epi, acc, reinterpret_cast<u16*>(smem) + wave * (128 * 64), mbase,
+  big_epilogue<Epi, MR>(epi, acc, reinterpret_cast<u16*>(smem) + wave * (128 * 64), mbase,
                nbase, lane, M, N, g);
 }
 
@@ -1392,8 +1398,6 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                          epi);
       return (int)hipGetLastError();
     }
-    const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
-    dim3 grid((unsigned)tiles, (unsigned)groups);
     // 8-phase pipeline when K splits into pairs of 64-deep tiles
     // (CADENCE_GEMM_P8=0 keeps the 2-buffer schedule for A/B runs)
     // (an A/B of the guide's two-barrier phase -- reads, barrier, lgkmcnt(0),
@@ -1403,9 +1407,37 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
       return e && e[0] == '0';
     }();
     const bool p8 = !p8_off && K % (2 * BK) == 0;
+    // tile height: 256 or 224 rows, whichever needs fewer (rounds x rows) on
+    // the CUs (M = 10208 = 32 x 319: 460 tiles of 224 in 2 rounds beat 400 of
+    // 256 in 2 rounds by 12.5 %); CADENCE_GEMM_BM=256|224 forces one
+    static const int bm_force = [] {
+      const char* e = getenv("CADENCE_GEMM_BM");
+      return e ? atoi(e) : 0;
+    }();
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          n <= 0)
+        n = 256;
+      return n;
+    }();
+    const int64_t ntn = (N + 255) / 256;
+    auto rounds_x_rows = [&](int64_t bm) {
+      const int64_t t = ((M + bm - 1) / bm) * ntn * groups;
+      return ((t + cus - 1) / cus) * bm;
+    };
+    const bool bm224 = p8 && (bm_force == 224 ||
+                              (bm_force != 256 && rounds_x_rows(224) < rounds_x_rows(256)));
+    const int64_t bm = bm224 ? 224 : 256;
+    const int64_t tiles = ((M + bm - 1) / bm) * ntn;
+    dim3 grid((unsigned)tiles, (unsigned)groups);
     if constexpr (std::is_same_v<Epi, EpiLinear>) {
 #define CADENCE_BIG_ACT(ACT_)                                                          \
-  if (p8) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 1>), grid,         \
+  if (bm224) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 1, 7>), grid,     \
+                             dim3(512), 0, st, A, lda, W, ldw, (int)M, (int)N, (int)K,  \
+                             a_goff, w_goff, EpiLinearA<ACT_>{epi});                    \
+  else if (p8) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 1>), grid,         \
                              dim3(512), 0, st, A, lda, W, ldw, (int)M, (int)N, (int)K,  \
                              a_goff, w_goff, EpiLinearA<ACT_>{epi});                    \
   else hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 0>), grid, dim3(512),      \
@@ -1419,6 +1451,9 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
         default: return (int)hipErrorInvalidValue;
       }
 #undef CADENCE_BIG_ACT
+    } else if (bm224) {
+      hipLaunchKernelGGL((gemm_big_kernel<Epi, 1, 7>), grid, dim3(512), 0, st, A, lda, W,
+                         ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
     } else if (p8) {
       hipLaunchKernelGGL((gemm_big_kernel<Epi, 1>), grid, dim3(512), 0, st, A, lda, W,
                          ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
