@@ -17,10 +17,19 @@
 // :85-86,149-151 (timm not vendored).
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include "common.hpp"
 #include "../../include/cadence_kernels.h"
 
 namespace {
+
+// V^T columns are stored in the P^T slot order of each 32-key group (slot
+// 8g + j <-> key 4g + j for j < 4, 16 + 4g + j - 4 for j >= 4), so a lane's 8
+// keys of a PV k-step are one 16-B run.  vslot(k) for a key k = 4q.
+CADENCE_DEV int vslot(int k) {
+  const int k0 = k & 31;
+  return (k & ~31) + (k0 < 16 ? 8 * (k0 >> 2) : 8 * ((k0 - 16) >> 2) + 4);
+}
 
 // K image: KW stored 16-B chunks per key row, XOR-swizzled so that the
 // 16-lane ds_read_b128 groups of a k-step are conflict-free (checked
@@ -47,7 +56,7 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
   constexpr int KS = HDK / 32;
   constexpr int NDT = HDV / 16;
   constexpr int VCH = VR / 8;         // stored V^T row groups of 8 dims
-  constexpr int VTS = NPMAX + 8;      // V^T row stride (elements): 16-B pad
+  constexpr int VTS = NPMAX + 16;     // V^T row stride: 32-B pad (b128 reads conflict-free)
   constexpr int KIMG = NPMAX * CPR;   // uint4 of the K image
   static_assert(KW % 2 == 0 && KW >= 8 && KW * 8 <= HDK && VR % 8 == 0, "layout");
   // one LDS array (K image, then V^T)
@@ -90,7 +99,7 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
       const int sh = (i & 1) * 16;
       const uint32_t e0 = (w[0][i >> 1] >> sh) & 0xffffu, e1 = (w[1][i >> 1] >> sh) & 0xffffu;
       const uint32_t e2 = (w[2][i >> 1] >> sh) & 0xffffu, e3 = (w[3][i >> 1] >> sh) & 0xffffu;
-      *reinterpret_cast<uint2*>(&vt[(dc * 8 + i) * VTS + kq * 4]) =
+      *reinterpret_cast<uint2*>(&vt[(dc * 8 + i) * VTS + vslot(kq * 4)]) =
           make_uint2(e0 | (e1 << 16), e2 | (e3 << 16));
     }
   }
@@ -141,9 +150,11 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
     // running max updated only when it grows by more than 2^8 (deferred
     // rescale: P <= 256 is exact enough in bf16, l and O stay fp32).
     constexpr float kThr = 8.0f;
-    for (int c0 = 0; c0 < np; c0 += 64) {
-      const bool two = c0 + 32 >= np;        // 32-key tail chunk
-      const bool mask = c0 + 64 > N;
+    // one 64-key chunk; MASK / TWO (32-key tail) only on the last chunk, so
+    // the full chunks carry no masking code
+    auto chunk = [&](int c0, auto mask_tag, auto two_tag) {
+      constexpr bool mask = decltype(mask_tag)::value;
+      constexpr bool two = decltype(two_tag)::value;
       f32x4 s[QT][4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -217,16 +228,23 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
           const int vrow = min(dt * 16 + c16, VR - 1);   // rows >= VR: discarded dims
-          const u16* vr = vt + vrow * VTS + c0 + 32 * kk + 4 * g;
-          const uint2 lo = *reinterpret_cast<const uint2*>(vr);
-          const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+          const bf16x8 vf = __builtin_bit_cast(
+              bf16x8, *reinterpret_cast<const uint4*>(vt + vrow * VTS + c0 + 32 * kk + 8 * g));
 #pragma unroll
           for (int u = 0; u < QT; ++u)
             o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[u][kk], o[u][dt], 0, 0, 0);
         }
       }
+    };
+    using F = std::false_type;
+    using T = std::true_type;
+    int c0 = 0;
+    for (; c0 + 64 <= N; c0 += 64) chunk(c0, F{}, F{});
+    if (c0 < N) {
+      if (c0 + 32 >= np) chunk(c0, T{}, T{});
+      else chunk(c0, T{}, F{});
     }
+
 #pragma unroll
     for (int u = 0; u < QT; ++u) {
       float lt = l[u];
