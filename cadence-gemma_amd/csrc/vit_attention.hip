@@ -64,7 +64,20 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
   uint4* kimg = smem;
   u16* vt = reinterpret_cast<u16*>(smem + KIMG);
 
-  const int h = blockIdx.x, b = blockIdx.y;
+  // XCD-aware (image, head) order: workgroups are dispatched round-robin
+  // over the 8 XCDs, so remap the dispatch index (bijectively) to give each
+  // XCD a contiguous range of images -- all heads of an image then share
+  // one L2 for the image's q|k|v rows (SigLIP's 144-B head slices straddle
+  // 128-B lines shared by neighbouring heads).
+  int h, b;
+  {
+    const int nh = gridDim.x, total = nh * gridDim.y;
+    const int lin = blockIdx.x + blockIdx.y * nh;
+    const int xcd = lin & 7, q8 = total >> 3, r8 = total & 7;
+    const int p = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (lin >> 3);
+    h = p % nh;
+    b = p / nh;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int D = H * hd;
   const int64_t rs = 3 * (int64_t)D;  // qkv row stride: [q | k | v] per token
