@@ -244,8 +244,10 @@ def main():
 
   result = None
   if rank == 0:
-    # dominant kernel: the single-kernel key with the most time in the step
-    gemm_keys = [k for k in ksum if k.startswith("gemm_big_kernel") and "+" not in k]
+    # dominant kernel: the single-stream GEMM key with the most time in the
+    # step (ViT-tower launches share the GPU between two streams: their keys
+    # carry a " [vit, 2 streams]" suffix and are reported, not ranked)
+    gemm_keys = [k for k in ksum if k.startswith("gemm_big_kernel") and "[" not in k]
     dom = max(gemm_keys, key=lambda k: ksum[k]["total_ms"]) if gemm_keys else None
     dec = None
     if decode_ms:

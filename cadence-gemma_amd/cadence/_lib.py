@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -30,6 +30,7 @@ F32 = ctypes.c_float
 _SIGS: dict[str, list] = {
     "cadence_abi_version": [],
     "cadence_gemm_workspace_bytes": [I64, I64, I64, I64],
+    "cadence_gemm_tile_rows": [I64, I64, I64, I64],
     "cadence_gemm_linear": [P, I64, P, I64, P, P, I64, P, I64, I64, I64, I64,
                             I32, I64, I64, I64, P, I64, P],
     "cadence_gemm_gated_gelu": [P, I64, P, I64, P, P, P, I64, I64, I64, I64, P,

@@ -13,6 +13,7 @@ what the modules call; they route through `torch.ops.cadence`.
 
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import NamedTuple
 
@@ -71,9 +72,21 @@ class KernelTimer:
   def __init__(self):
     self.enabled = False
     self.records: dict[str, list] = {}
+    self.scope = ""
 
   def reset(self):
     self.records = {}
+
+  @contextlib.contextmanager
+  def scoped(self, suffix: str):
+    """Records inside get `suffix` appended to their key (the ViT towers run
+    on two streams, so their per-launch event windows include time shared
+    with the other tower: kept apart from the single-stream launches)."""
+    prev, self.scope = self.scope, suffix
+    try:
+      yield
+    finally:
+      self.scope = prev
 
   def start(self, t: torch.Tensor):
     if not self.enabled or torch.cuda.is_current_stream_capturing():
@@ -87,7 +100,7 @@ class KernelTimer:
       return
     end = torch.cuda.Event(enable_timing=True)
     end.record(torch.cuda.current_stream(t.device))
-    self.records.setdefault(key, []).append((ev, end, float(work)))
+    self.records.setdefault(key + self.scope, []).append((ev, end, float(work)))
 
   def summary(self) -> dict[str, dict]:
     torch.cuda.synchronize()
@@ -106,6 +119,14 @@ TIMER = KernelTimer()
 
 def _tile(M: int) -> bool:
   return M > 64
+
+
+def _big_key(epi: str, M: int, N: int, K: int, groups: int = 1) -> str:
+  """The rocprof name of the prefill GEMM kernel a launch runs:
+  gemm_big_kernel<Epi, P8, MR> (tile height 32 MR, cadence_gemm_tile_rows)."""
+  rows = _lib.load().cadence_gemm_tile_rows(M, N, K, groups)
+  p8 = 1 if (K % 128 == 0 and os.environ.get("CADENCE_GEMM_P8", "1") != "0") else 0
+  return f"gemm_big_kernel<{epi}, {p8}, {rows // 32}>"
 
 
 _COUNTERS: dict[int, torch.Tensor] = {}
@@ -257,7 +278,8 @@ def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off,
   _lib.check(_lib.load().cadence_gemm_linear(
       _p(a), lda, _p(w), ldw, _p(bias), _p(resid), ldr, _p(out), ldo, M, N, K,
       act, row_div, row_mul, row_off, _p(ws), nws, _s(a)), "gemm_linear")
-  TIMER.stop(ev, f"gemm_big_kernel<EpiLinearA<{act}>>", 2.0 * M * N * K, a)
+  if ev is not None:
+    TIMER.stop(ev, _big_key(f"EpiLinearA<{act}>", M, N, K), 2.0 * M * N * K, a)
 
 
 @_reg("gemm_linear_conv1d_(Tensor a, Tensor w, Tensor? bias, Tensor conv_w, "
@@ -318,7 +340,7 @@ def _gemm_linear_rmsnorm(a, w, bias, resid, scale, eps, w_packed=False,
     _lib.check(lib.cadence_gemm_linear(
         _p(a), lda, _p(w), ldw, _p(bias), _p(resid), ldr, _p(out), N, M, N, K,
         0, M, 0, 0, _p(ws), nws, _s(a)), "gemm_linear")
-    TIMER.stop(ev, "gemm_big_kernel<EpiLinearA<0>>", 2.0 * M * N * K, a)
+    TIMER.stop(ev, _big_key("EpiLinearA<0>", M, N, K), 2.0 * M * N * K, a)
     _lib.check(lib.cadence_rmsnorm(_p(out), N, _p(scale), _p(nout),
                                    0 if norm_packed else N, M, N, float(eps), _s(a)),
                "rmsnorm")
@@ -352,7 +374,8 @@ def _gated_gelu(a, w_packed, bias_gate, bias_up, decode_layout=False, a_rows=-1,
       _p(a), lda, _p(w_packed), 0 if decode_layout else K, _p(bias_gate),
       _p(bias_up), _p(out), 0 if out_packed else F, M, F, K, _p(ws), nws, _s(a)),
       "gated_gelu")
-  TIMER.stop(ev, "gemm_big_kernel<EpiGatedGelu>", 4.0 * M * F * K, a)
+  if ev is not None:
+    TIMER.stop(ev, _big_key("EpiGatedGelu", M, 2 * F, K), 4.0 * M * F * K, a)
   return out
 
 
@@ -375,7 +398,9 @@ def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos,
       _p(bias_a), _p(softplus_a), _p(segment_pos.contiguous()), _p(a), _p(nx),
       E, M, H, bw, _p(ws), nws,
       _s(x)), "rglru_gates")
-  TIMER.stop(ev, "gemm_big_kernel<EpiRglruGates>", 2.0 * M * 2 * bw * bw * H, x)
+  if ev is not None:
+    TIMER.stop(ev, _big_key("EpiRglruGates", M, 2 * bw, bw, H),
+               2.0 * M * 2 * bw * bw * H, x)
   return a, nx
 
 
@@ -416,7 +441,8 @@ def _vit_residual(a, w, bias, gamma, resid):
   _lib.check(_lib.load().cadence_gemm_vit_residual(
       _p(a), lda, _p(w), ldw, _p(bias), _p(gamma), _p(resid), ldr, M, N, K,
       _p(ws), nws, _s(a)), "vit_residual")
-  TIMER.stop(ev, "gemm_big_kernel<EpiVitResid>", 2.0 * M * N * K, a)
+  if ev is not None:
+    TIMER.stop(ev, _big_key("EpiVitResid", M, N, K), 2.0 * M * N * K, a)
 
 
 @_reg("patch_embed_(Tensor patches, Tensor w, Tensor bias, Tensor pos, "

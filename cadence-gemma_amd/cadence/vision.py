@@ -242,11 +242,12 @@ class VisionEncoder(nn.Module):
     cur = torch.cuda.current_stream(pixels.device)
     side = self._side_stream(pixels.device)
     side.wait_stream(cur)
-    with torch.cuda.stream(side):
-      self.siglip.features_into(pixels, out2d, self.config.dino.width, n)
-    pixels.record_stream(side)
-    out2d.record_stream(side)
-    self.dino.features_into(pixels, out2d, 0, n)
+    with ops.TIMER.scoped(" [vit, 2 streams]"):
+      with torch.cuda.stream(side):
+        self.siglip.features_into(pixels, out2d, self.config.dino.width, n)
+      pixels.record_stream(side)
+      out2d.record_stream(side)
+      self.dino.features_into(pixels, out2d, 0, n)
     cur.wait_stream(side)
 
   def encode(self, pixels: torch.Tensor) -> torch.Tensor:

@@ -1378,6 +1378,43 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
 #undef CADENCE_STREAM
 }
 
+// Prefill engine plan for M > kSkinnyMaxM: 0 = 2-buffer 256-row kernel,
+// 256 / 224 = 8-phase kernel with that tile height.
+//  * 8-phase when K splits into pairs of 64-deep tiles (CADENCE_GEMM_P8=0
+//    keeps the 2-buffer schedule for A/B runs; an A/B of the guide's
+//    two-barrier phase -- reads, barrier, lgkmcnt(0), MFMAs, barrier -- ran
+//    1-5 % slower on every prefill shape);
+//  * tile height 256 or 224 rows, whichever needs fewer (rounds x rows) on
+//    the CUs (M = 10208 = 32 x 319: 460 tiles of 224 in 2 rounds beat 400 of
+//    256 in 2 rounds); CADENCE_GEMM_BM=256|224 forces one.
+int big_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
+  static const bool p8_off = [] {
+    const char* e = getenv("CADENCE_GEMM_P8");
+    return e && e[0] == '0';
+  }();
+  static const int bm_force = [] {
+    const char* e = getenv("CADENCE_GEMM_BM");
+    return e ? atoi(e) : 0;
+  }();
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    return n;
+  }();
+  if (p8_off || K % (2 * BK) != 0) return 0;
+  const int64_t ntn = (N + 255) / 256;
+  auto rounds_x_rows = [&](int64_t bm) {
+    const int64_t t = ((M + bm - 1) / bm) * ntn * groups;
+    return ((t + cus - 1) / cus) * bm;
+  };
+  if (bm_force == 224) return 224;
+  if (bm_force != 256 && rounds_x_rows(224) < rounds_x_rows(256)) return 224;
+  return 256;
+}
+
 template <class Epi>
 int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                 int64_t N, int64_t K, int64_t groups, int64_t a_goff,
@@ -1398,39 +1435,11 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                          epi);
       return (int)hipGetLastError();
     }
-    // 8-phase pipeline when K splits into pairs of 64-deep tiles
-    // (CADENCE_GEMM_P8=0 keeps the 2-buffer schedule for A/B runs)
-    // (an A/B of the guide's two-barrier phase -- reads, barrier, lgkmcnt(0),
-    // MFMAs, barrier -- ran 1-5 % slower on every prefill shape)
-    static const bool p8_off = [] {
-      const char* e = getenv("CADENCE_GEMM_P8");
-      return e && e[0] == '0';
-    }();
-    const bool p8 = !p8_off && K % (2 * BK) == 0;
-    // tile height: 256 or 224 rows, whichever needs fewer (rounds x rows) on
-    // the CUs (M = 10208 = 32 x 319: 460 tiles of 224 in 2 rounds beat 400 of
-    // 256 in 2 rounds by 12.5 %); CADENCE_GEMM_BM=256|224 forces one
-    static const int bm_force = [] {
-      const char* e = getenv("CADENCE_GEMM_BM");
-      return e ? atoi(e) : 0;
-    }();
-    static const int cus = [] {
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-          n <= 0)
-        n = 256;
-      return n;
-    }();
-    const int64_t ntn = (N + 255) / 256;
-    auto rounds_x_rows = [&](int64_t bm) {
-      const int64_t t = ((M + bm - 1) / bm) * ntn * groups;
-      return ((t + cus - 1) / cus) * bm;
-    };
-    const bool bm224 = p8 && (bm_force == 224 ||
-                              (bm_force != 256 && rounds_x_rows(224) < rounds_x_rows(256)));
+    const int rows = big_tile_rows(M, N, K, groups);
+    const bool p8 = rows != 0;
+    const bool bm224 = rows == 224;
     const int64_t bm = bm224 ? 224 : 256;
-    const int64_t tiles = ((M + bm - 1) / bm) * ntn;
+    const int64_t tiles = ((M + bm - 1) / bm) * ((N + 255) / 256);
     dim3 grid((unsigned)tiles, (unsigned)groups);
     if constexpr (std::is_same_v<Epi, EpiLinear>) {
 #define CADENCE_BIG_ACT(ACT_)                                                          \
@@ -1514,7 +1523,13 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 6; }
+int cadence_abi_version(void) { return 7; }
+
+int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
+  if (M <= kSkinnyMaxM || M <= 0) return 0;
+  const int r = big_tile_rows(M, N, K, groups > 0 ? groups : 1);
+  return r ? r : 256;
+}
 
 int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
                                      int64_t groups) {
