@@ -768,13 +768,15 @@ def _splice_positions(text_pos, n_vis):
 
 
 @_reg("decode_advance_(Tensor next_token, Tensor(a!) tokens_out, "
-      "Tensor(b!) step, Tensor(c!) positions) -> ()")
-def _decode_advance(next_token, tokens_out, step, positions):
+      "Tensor(b!) step, Tensor(c!) positions, Tensor(d!)? cur=None) -> ()")
+def _decode_advance(next_token, tokens_out, step, positions, cur=None):
   B = next_token.numel()
   _need(tokens_out.dtype == _I32 and tokens_out.stride(1) == 1, "tokens_out")
+  if cur is not None:
+    _need(cur.dtype == _I32 and cur.is_contiguous() and cur.numel() == B, "cur")
   _lib.check(_lib.load().cadence_decode_advance(
       _p(next_token), _p(tokens_out), tokens_out.stride(0), _p(step),
-      _p(positions), B, _s(next_token)), "decode_advance")
+      _p(positions), _p(cur), B, _s(next_token)), "decode_advance")
 
 
 # ----------------------------------------------------------------- helpers

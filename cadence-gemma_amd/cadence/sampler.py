@@ -271,8 +271,7 @@ class _DecodeGraph:
   def _step(self):
     nxt, _, _ = self.model.next_token(self.cur[:, None], self.pos[:, None],
                                       self.cache, False, inplace=True)
-    ops.ops.decode_advance_(nxt, self.buf, self.step, self.pos)
-    self.cur.copy_(nxt)
+    ops.ops.decode_advance_(nxt, self.buf, self.step, self.pos, self.cur)
 
   def run(self, cache, cur, pos, buf, step, n_more, all_done=None, events=None):
     dev_stream = torch.cuda.current_stream(cur.device)

@@ -1052,11 +1052,16 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
 
 // One block: 64 output columns x MS rows over one K split; 4 waves split the
 // K range round-robin in 32-deep steps and are summed through LDS.
-template <int MS>
+template <int MS, bool ARGMAX = false>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
     int64_t ldw, int M, int N, int K, int klen, float* __restrict__ part,
-    int64_t a_goff, int64_t w_goff, int packed) {
+    int64_t a_goff, int64_t w_goff, int packed, float cap = 0.0f,
+    u16* __restrict__ logits = nullptr, float* __restrict__ bval = nullptr,
+    int* __restrict__ bidx = nullptr) {
+  // ARGMAX (one K split): the logits epilogue runs here -- rounding,
+  // soft-cap, optional bf16 logits, and the (max, lowest index) of this
+  // block's 64 columns per row -- instead of fp32 partials + a reduce launch
   constexpr int MR = MS / 16;
   constexpr int UNROLL = 2;
   __shared__ float red[4][MS * 64];
@@ -1116,6 +1121,28 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(
       for (int r = 0; r < 4; ++r)
         red[wave][(i * 16 + rsub + r) * 64 + j * 16 + csub] = acc[i][j][r];
   __syncthreads();
+  if constexpr (ARGMAX) {
+    // 64 consecutive idx = one row, one wave: lane = column
+    for (int idx = tid; idx < MS * 64; idx += 256) {
+      const int m = idx / 64, n = idx % 64;
+      if (m >= M) continue;   // wave-uniform
+      float l = rbf((red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx]));
+      if (cap > 0.0f) l = softcap(l, cap);
+      if (logits) logits[(int64_t)m * N + n0 + n] = f2bf(l);
+      float v = l;
+      int ix = n0 + n;
+      for (int off = 32; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(v, off, 64);
+        const int oi = __shfl_xor(ix, off, 64);
+        if (ov > v || (ov == v && oi < ix)) { v = ov; ix = oi; }
+      }
+      if (n == 0) {
+        bval[(int64_t)m * gridDim.x + blockIdx.x] = v;
+        bidx[(int64_t)m * gridDim.x + blockIdx.x] = ix;
+      }
+    }
+    return;
+  }
   float* dst = part + ((int64_t)blockIdx.y * gridDim.z + g) * (int64_t)M * N;
   for (int idx = tid; idx < MS * 64; idx += 256) {
     const int m = idx / 64, n = idx % 64;
@@ -1523,7 +1550,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 7; }
+int cadence_abi_version(void) { return 8; }
 
 int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
   if (M <= kSkinnyMaxM || M <= 0) return 0;
@@ -1754,10 +1781,30 @@ int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
   float* part = static_cast<float*>(scratch);
   const int64_t nblk = (V + 255) / 256;
   float* bval = part + (int64_t)splits * M * V;
-  int* bidx = reinterpret_cast<int*>(bval + M * nblk);
+  int* bidx = reinterpret_cast<int*>(bval + M * nblk);   // split path
   const u16* A = static_cast<const u16*>(X);
   const u16* W = static_cast<const u16*>(E);
   dim3 grid((unsigned)(V / 64), (unsigned)splits, 1);
+  if (splits == 1) {
+    // one pass: the skinny kernel emits per-64-column (max, index) pairs
+    // (into the partial-slab area of the scratch, unused without a split)
+    const int64_t nb64 = V / 64;
+    u16* lo = static_cast<u16*>(logits_out);
+    bval = part;
+    bidx = reinterpret_cast<int*>(part + M * nb64);
+#define CADENCE_LGA(MS_)                                                                 \
+  hipLaunchKernelGGL((gemm_skinny_kernel<MS_, true>), grid, dim3(256), 0, st, A, ldx, W, \
+                     lde, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0, \
+                     packed, soft_cap, lo, bval, bidx)
+    if (M <= 16) CADENCE_LGA(16);
+    else if (M <= 32) CADENCE_LGA(32);
+    else CADENCE_LGA(64);
+#undef CADENCE_LGA
+    if (next_token)
+      hipLaunchKernelGGL(argmax_final_kernel, dim3((unsigned)M), dim3(256), 0, st,
+                         bval, bidx, (int)nb64, next_token);
+    return (int)hipGetLastError();
+  }
   if (M <= 16)
     hipLaunchKernelGGL((gemm_skinny_kernel<16>), grid, dim3(256), 0, st, A, ldx, W,
                        lde, (int)M, (int)V, (int)D, (int)klen, part, (int64_t)0, (int64_t)0,

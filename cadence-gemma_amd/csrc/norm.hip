@@ -177,12 +177,15 @@ __global__ void segment_info_kernel(const int32_t* __restrict__ pos,
 __global__ void decode_advance_kernel(const int32_t* __restrict__ next,
                                       int32_t* __restrict__ out, int64_t ldo,
                                       int32_t* __restrict__ step,
-                                      int32_t* __restrict__ pos, int B) {
+                                      int32_t* __restrict__ pos,
+                                      int32_t* __restrict__ cur, int B) {
   const int b = blockIdx.x * 256 + threadIdx.x;
   const int s = *step;
   if (b < B) {
-    out[(int64_t)b * ldo + s] = next[b];
+    const int32_t t = next[b];
+    out[(int64_t)b * ldo + s] = t;
     pos[b] += 1;
+    if (cur) cur[b] = t;
   }
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) *step = s + 1;
@@ -194,12 +197,12 @@ extern "C" {
 
 int cadence_decode_advance(const int32_t* next_token, int32_t* tokens_out,
                            int64_t ld_out, int32_t* step, int32_t* positions,
-                           int64_t B, void* stream) {
+                           int32_t* cur_out, int64_t B, void* stream) {
   if (B <= 0) return 0;
   if (B > 256) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(256), 0,
                      static_cast<hipStream_t>(stream), next_token, tokens_out,
-                     ld_out, step, positions, (int)B);
+                     ld_out, step, positions, cur_out, (int)B);
   return (int)hipGetLastError();
 }
 

@@ -331,10 +331,11 @@ int cadence_splice_positions(const int32_t* text_pos, int32_t* out,
 
 /* Greedy decode bookkeeping (the host loop of examples/cadence_sampler.py:
  * 131-151 moved on device): tokens_out[b, *step] = next_token[b];
- * positions[b] += 1; *step += 1.  B <= 256. */
+ * positions[b] += 1; *step += 1; cur_out[b] = next_token[b] (the next
+ * step's input token; cur_out may be null).  B <= 256. */
 int cadence_decode_advance(const int32_t* next_token, int32_t* tokens_out,
                            int64_t ld_out, int32_t* step, int32_t* positions,
-                           int64_t B, void* stream);
+                           int32_t* cur_out, int64_t B, void* stream);
 
 #ifdef __cplusplus
 }  // extern "C"
