@@ -251,8 +251,10 @@ def main():
     dom = max(gemm_keys, key=lambda k: ksum[k]["total_ms"]) if gemm_keys else None
     dec = None
     if decode_ms:
-      # replayed steps 2..decode: context n_vis + prompt + i for step i
-      ctx = [n_vis + args.prompt + i for i in range(1, args.decode)]
+      # replayed steps: the last `decode_steps` of the prompt-token step +
+      # decode steps; step i attends to n_vis + prompt + i keys
+      dsteps = ev_list[0]["decode_steps"]
+      ctx = [n_vis + args.prompt + i for i in range(args.decode - dsteps, args.decode)]
       nbytes = decode_hbm_bytes(model, cfg, args.batch, ctx,
                                 cfg.attention_window_size)
       us = sum(decode_ms) / len(decode_ms) * 1e3

@@ -130,12 +130,28 @@ class Sampler:
       events["prefill_start"] = torch.cuda.Event(enable_timing=True)
       events["prefill_end"] = torch.cuda.Event(enable_timing=True)
       events["prefill_start"].record()
+    # greedy, no logits: the last prompt token's cached step is the first
+    # replay of the decode graph (no eager ~200-launch step)
+    graph_first = (t > 1 and self.use_graph and self.greedy_sampling and
+                   not return_logits and steps > 2)
     if t > 1:
       prev_logits, cache = self.apply_model(tokens[:, :-1], positions[:, :-1],
                                             None, return_logits and echo, True,
                                             img_path, images)
       if events is not None:
         events["prefill_end"].record()
+      if graph_first:
+        buf = torch.full((b, steps), self.vocab.pad_id(), dtype=torch.int32,
+                         device=dev)
+        pos = positions[:, -1].to(torch.int32).contiguous()
+        step = torch.zeros(1, dtype=torch.int32, device=dev)
+        cur = tokens[:, -1].to(torch.int32).contiguous()
+        self._decode_graph(cur, pos, cache, buf, step, steps,
+                           end_sampling_at_eos_token, events, start=0)
+        if echo:
+          buf = torch.cat([tokens, buf], dim=1)
+        return SamplingState(buf, step, torch.tensor(steps), pos[:, None], cache,
+                             torch.zeros(b, dtype=torch.bool), None)
       nxt, logits, cache = model.next_token(tokens[:, -1:], positions[:, -1:],
                                             cache, return_logits)
     else:
@@ -197,7 +213,7 @@ class Sampler:
     return bool((buf == self.vocab.eos_id()).any(dim=1).all())
 
   def _decode_graph(self, cur, pos, cache, buf, step, n_more, eos_stop,
-                    events=None):
+                    events=None, start=1):
     """Replays a captured single-token decode step `n_more` times."""
     key = (cur.shape[0], cur.device)
     eng = self._graphs.get(key) if hasattr(self, "_graphs") else None
@@ -208,7 +224,7 @@ class Sampler:
                          cur.device)
       self._graphs[key] = eng
     eng.run(cache, cur, pos, buf, step, n_more,
-            (lambda b: self._all_done(b)) if eos_stop else None, events)
+            (lambda b: self._all_done(b)) if eos_stop else None, events, start)
 
   # ------------------------------------------------------------------- API
 
@@ -273,14 +289,17 @@ class _DecodeGraph:
                                       self.cache, False, inplace=True)
     ops.ops.decode_advance_(nxt, self.buf, self.step, self.pos, self.cur)
 
-  def run(self, cache, cur, pos, buf, step, n_more, all_done=None, events=None):
+  def run(self, cache, cur, pos, buf, step, n_more, all_done=None, events=None,
+          start=1):
+    """Replays the step `n_more` times from buffer column `start` (the
+    tokens before it are already in `buf`)."""
     dev_stream = torch.cuda.current_stream(cur.device)
     for name, c in cache.items():
       for dst, src in zip(self.cache[name], c):
         dst.copy_(src)
     self.cur.copy_(cur)
     self.pos.copy_(pos)
-    self.step.fill_(1)
+    self.step.fill_(start)
     self.stream.wait_stream(dev_stream)
     with torch.cuda.stream(self.stream):
       if events is not None:   # the replays alone (cache copies excluded)
@@ -297,7 +316,7 @@ class _DecodeGraph:
         events["decode_end"].record()
     dev_stream.wait_stream(self.stream)
     steps = buf.shape[1]
-    buf[:, 1:].copy_(self.buf[:, 1:steps])
+    buf[:, start:].copy_(self.buf[:, start:steps])
     step.copy_(self.step)
     pos.copy_(self.pos)
     cur.copy_(self.cur)
