@@ -1346,6 +1346,27 @@ int stream_plan(int64_t M, int64_t K, int* ksw, int* splits) {
   return 1;
 }
 
+// Decode residual GEMM feeding an RMSNorm: the split-K plan whose row-owned
+// reduce kernel also does the norm.  K > 2560 is split anyway; a one-split
+// K (the 2560-wide output projections) is split in two as well: 32
+// columns x one K half per workgroup halve the activation bytes each
+// workgroup pulls, and the reduce kernel replaces the norm launch (decode
+// step -50 us; CADENCE_OUTPROJ_SPLIT=1 keeps one split for A/B runs).
+int rmsnorm_stream_plan(int64_t M, int64_t K, int* ksw, int* splits) {
+  static const bool split2 = [] {
+    const char* e = getenv("CADENCE_OUTPROJ_SPLIT");
+    return !(e && e[0] == '1');
+  }();
+  if (!stream_plan(M, K, ksw, splits)) return 0;
+  if (*splits >= 2 && *splits <= 4) return 1;
+  if (split2 && *splits == 1 && *ksw == 10 && K == 2560) {
+    *ksw = 5;
+    *splits = 2;
+    return 1;
+  }
+  return 0;
+}
+
 // CADENCE_GEMM_LEGACY=1 selects the 128x128 register-staged tile kernel
 // (A/B comparisons in one binary).
 bool use_legacy_tile() {
@@ -1379,7 +1400,7 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
                    int splits, float* parts, int packed, hipStream_t st) {
   // two column tiles per workgroup when that still leaves >= 150 workgroups
   // (cold-weight sweep, tools/gemv_lab.py: xy 12.7 -> 8.9 us, down 18.6 -> 13)
-  const int ntw = (!Epi::kPaired && ksw == 10 && N % 32 == 0 &&
+  const int ntw = (!Epi::kPaired && (ksw == 10 || ksw == 5) && N % 32 == 0 &&
                    (N / 32) * splits * groups >= 150) ? 2 : 1;
   const unsigned nblk = (unsigned)(Epi::kPaired ? N / 32 : N / 16 / ntw);
   const int64_t ks = K / 32;
@@ -1393,12 +1414,14 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
     if (ksw == 1) CADENCE_STREAM(16, 1, 1);
     else if (ksw == 2) CADENCE_STREAM(16, 2, 1);
     else if (ksw == 4) CADENCE_STREAM(16, 4, 1);
+    else if (ksw == 5) { if constexpr (std::is_same_v<Epi, EpiLinear>) CADENCE_STREAM(16, 5, 2); }
     else if (ntw == 2) { if constexpr (!Epi::kPaired) CADENCE_STREAM(16, 10, 2); }
     else CADENCE_STREAM(16, 10, 1);
   } else {
     if (ksw == 1) CADENCE_STREAM(32, 1, 1);
     else if (ksw == 2) CADENCE_STREAM(32, 2, 1);
     else if (ksw == 4) CADENCE_STREAM(32, 4, 1);
+    else if (ksw == 5) { if constexpr (std::is_same_v<Epi, EpiLinear>) CADENCE_STREAM(32, 5, 2); }
     else if (ntw == 2) { if constexpr (!Epi::kPaired) CADENCE_STREAM(32, 10, 2); }
     else CADENCE_STREAM(32, 10, 1);
   }
@@ -1623,8 +1646,7 @@ int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
 
 int64_t cadence_gemm_rmsnorm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   int ksw = 0, ss = 0;
-  if (M <= 0 || N > 4096 || !stream_plan(M, K, &ksw, &ss) || ss < 2 || ss > 4)
-    return 0;
+  if (M <= 0 || N > 4096 || N % 64 || !rmsnorm_stream_plan(M, K, &ksw, &ss)) return 0;
   return (int64_t)ss * M * N * 4;
 }
 
@@ -1645,11 +1667,9 @@ int cadence_gemm_linear_rmsnorm(const void* A, int64_t lda, const void* W,
                 static_cast<const u16*>(resid), ld_resid, 0,
                 RowMap{M, 0, 0}, 0.0f};
   int ksw = 0, ss = 0;
-  if (N <= 4096 && N % 64 == 0 && stream_plan(M, K, &ksw, &ss) && ss >= 2 &&
-      ss <= 4) {
-    // decode GEMM that is split-K anyway (K > 2560): the row-owned reduce +
+  if (N <= 4096 && N % 64 == 0 && rmsnorm_stream_plan(M, K, &ksw, &ss)) {
+    // decode GEMM split over K (rmsnorm_stream_plan): the row-owned reduce +
     // residual + RMSNorm kernel replaces the split-K reduce and the norm.
-    // (Forcing a split on a single-pass GEMM measured slower.)
     const int splits = ss;
     const int64_t need = (int64_t)splits * M * N * 4;
     if (!workspace || ws_bytes < need) return (int)hipErrorInvalidValue;

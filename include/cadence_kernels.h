@@ -105,7 +105,7 @@ int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
  * and ffw_down, each followed by the next norm; modules.py:908-913):
  *   out = A . W^T + bias + resid          (as cadence_gemm_linear, act 0)
  *   norm_out = RMSNorm(out; norm_scale)    (as cadence_rmsnorm)
- * For M <= 32 the GEMM runs split-K and one row-owned kernel finishes the
+ * For M <= 32 the GEMM runs split-K (K = 2560: 2 splits) and one row-owned kernel finishes the
  * reduction, the residual and the norm (workspace:
  * cadence_gemm_rmsnorm_workspace_bytes); otherwise GEMM + norm kernels. */
 int64_t cadence_gemm_rmsnorm_workspace_bytes(int64_t M, int64_t N, int64_t K);
