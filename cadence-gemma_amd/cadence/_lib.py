@@ -38,6 +38,8 @@ _SIGS: dict[str, list] = {
     "cadence_rglru_gates": [P, I64, P, I64, P, P, P, P, P, P, I64, I64, I64, I64,
                             P, I64, P],
     "cadence_gemm_rmsnorm_workspace_bytes": [I64, I64, I64],
+    "cadence_qkv_rope_decode": [P, I64, P, I64, P, P, P, P, I64, I64, I64, I64, P,
+                                I64, P],
     "cadence_gemm_linear_conv1d": [P, I64, P, I64, P, P, I64, I64, I64, I64, I64,
                                    P, P, P, I64, P],
     "cadence_gemm_linear_rmsnorm": [P, I64, P, I64, P, P, I64, P, I64, I64, I64,

@@ -73,6 +73,7 @@ class LocalAttentionBlock(nn.Module):
     self.proj_v = nn.Linear(width, self.head_dim, bias=False, **kw)
     self.proj_final = nn.Linear(width, width, bias=True, **kw)
     self._packed = PackCache()
+    self._packed_rope = PackCache()
     self.reset_parameters()
 
   @property
@@ -98,13 +99,25 @@ class LocalAttentionBlock(nn.Module):
         lambda: torch.cat([self.proj_q.weight, self.proj_k.weight,
                            self.proj_v.weight]).contiguous())
 
+  def qkv_weight_rope(self):
+    """[proj_q; proj_k; proj_v] in cadence_qkv_rope_decode's row order."""
+    return self._packed_rope.get(
+        [self.proj_q.weight, self.proj_k.weight, self.proj_v.weight],
+        lambda: self.qkv_weight()[ops.qkv_rope_permutation(
+            self.num_heads, self.head_dim, self.proj_q.weight.device)].contiguous())
+
   def fused(self, xn2d, pos, b, t, cache, return_cache, resid2d, norm=None):
     """Attention branch on normalised rows; returns (resid + out,
     norm(resid + out) or None, cache)."""
     h, hd = self.num_heads, self.head_dim
-    qkv = ops.linear(xn2d, self.qkv_weight())
-    q, k, v = ops.ops.rope_qkv(qkv, pos.view(-1), h, hd,
-                               ops.rope_table(qkv.device, hd))
+    if cache is not None and t == 1 and b <= 32 and self.width <= 2560:
+      # decode: RoPE runs in the q|k|v projection's epilogue
+      q, k, v = ops.qkv_rope_decode(xn2d, self.qkv_weight_rope(),
+                                    pos.view(-1).to(torch.int32), h, hd)
+    else:
+      qkv = ops.linear(xn2d, self.qkv_weight())
+      q, k, v = ops.ops.rope_qkv(qkv, pos.view(-1), h, hd,
+                                 ops.rope_table(qkv.device, hd))
     if cache is None:
       seg, start = ops.ops.segment_info(pos)
       enc = ops.ops.local_attention(q, k, v, seg, start, b, t, h, hd,

@@ -655,6 +655,43 @@ def _rope_qkv(qkv, positions, H, hd, table=None):
   return q, k, v
 
 
+@_reg("qkv_rope_decode(Tensor a, Tensor w_perm, Tensor positions, int H, int hd, "
+      "Tensor? table, bool w_packed=False, int a_rows=-1) -> (Tensor, Tensor, Tensor)")
+def _qkv_rope_decode(a, w_perm, positions, H, hd, table=None, w_packed=False,
+                     a_rows=-1):
+  """Decode q|k|v GEMV + RoPE; `w_perm` rows as qkv_rope_permutation()."""
+  ldw = _wld(w_perm, w_packed, "w_perm")
+  N, K = w_perm.shape[0], w_perm.shape[1]
+  _need(N == (H + 2) * hd, "w_perm rows")
+  if a_rows >= 0:
+    lda, M = 0, a_rows
+    _need(a.numel() == K * 16 * (-(-M // 16)), "a: packed rows size")
+  else:
+    lda = _mat(a, "a")
+    M = a.shape[0]
+  _need(positions.dtype == _I32 and positions.numel() == M, "positions")
+  q = torch.empty(M, H * hd, dtype=_BF16, device=a.device)
+  k = torch.empty(M, hd, dtype=_BF16, device=a.device)
+  v = torch.empty(M, hd, dtype=_BF16, device=a.device)
+  tlen = table.shape[0] if table is not None else 0
+  _lib.check(_lib.load().cadence_qkv_rope_decode(
+      _p(a), lda, _p(w_perm), ldw, _p(positions.contiguous()), _p(q), _p(k), _p(v),
+      M, H, hd, K, _p(table), tlen, _s(a)), "qkv_rope_decode")
+  return q, k, v
+
+
+def qkv_rope_permutation(H: int, hd: int, device=None) -> torch.Tensor:
+  """Row order of cadence_qkv_rope_decode's weight: in each of the H + 1
+  q / k heads, rows 2i, 2i + 1 <- dims i, i + hd/4 (i < hd/4)."""
+  perm = torch.arange((H + 2) * hd)
+  q4 = hd // 4
+  i = torch.arange(q4)
+  for h in range(H + 1):
+    perm[h * hd + 2 * i] = h * hd + i
+    perm[h * hd + 2 * i + 1] = h * hd + q4 + i
+  return perm.to(device) if device is not None else perm
+
+
 @_reg("local_attention(Tensor q, Tensor k, Tensor v, Tensor seg_id, "
       "Tensor seg_start, int B, int L, int H, int hd, int window) -> Tensor")
 def _local_attention(q, k, v, seg_id, seg_start, B, L, H, hd, window):
@@ -807,6 +844,16 @@ def linear(x2d, w, bias=None, act=0, resid=None, out=None,
   else:
     ops.gemm_linear_(a, w, bias, resid, out, act, div, mul, off, False, ar)
   return out
+
+
+def qkv_rope_decode(x2d, w_perm, positions, H, hd):
+  """Decode q, k, v (RoPE applied) from the permuted q|k|v weight."""
+  a, ar = _a(x2d)
+  wd = decode_weight(w_perm)
+  table = rope_table(w_perm.device, hd)
+  if wd is not None:
+    return ops.qkv_rope_decode(a, wd, positions, H, hd, table, True, ar)
+  return ops.qkv_rope_decode(a, w_perm, positions, H, hd, table, False, ar)
 
 
 def linear_conv1d_(x2d, w, bias, conv_w, conv_b, conv_state):

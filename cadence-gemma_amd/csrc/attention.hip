@@ -538,20 +538,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
 
 // ------------------------------------------------------------------- RoPE
 
-// One thread: 8 rotation pairs (16-B loads) of one head of one row, plus
-// the matching 16 pass-through dims.  Heads 0..H-1 are queries, head H is
-// the key; v is copied by head H's threads.
-// modules.py:73-81: fp32 inverse frequency (10000 ** (2i / rope_dim))^-1,
-// fp32 angle pos * inv, sin / cos rounded to the activation dtype.
-CADENCE_DEV void rope_sincos(int pos, int fi, int half, float& sn, float& cs) {
-  const float expo = (float)(2 * fi) / (float)half;
-  const float timescale = (float)pow(10000.0, (double)expo);
-  const float inv = 1.0f / timescale;
-  const float ang = (float)pos * inv;
-  sn = rbf((float)sin((double)ang));
-  cs = rbf((float)cos((double)ang));
-}
-
+// sin / cos table (common.hpp rope_sincos) for positions [0, P).
 __global__ __launch_bounds__(256) void rope_table_kernel(u16* __restrict__ t,
                                                          int P, int hd) {
   const int quarter = hd / 4, half = hd / 2;
@@ -565,6 +552,9 @@ __global__ __launch_bounds__(256) void rope_table_kernel(u16* __restrict__ t,
   }
 }
 
+// One thread: 8 rotation pairs (16-B loads) of one head of one row, plus
+// the matching 16 pass-through dims.  Heads 0..H-1 are queries, head H is
+// the key; v is copied by head H's threads.
 __global__ __launch_bounds__(256) void rope_qkv_kernel(
     const u16* __restrict__ qkv, int64_t ld, const int32_t* __restrict__ pos,
     u16* __restrict__ qo, u16* __restrict__ ko, u16* __restrict__ vo, int64_t M,

@@ -117,6 +117,18 @@ CADENCE_DEV int64_t xpk(int m, int k, int mt) {
           << 3) + (k & 7);
 }
 // Offset of row m, column k in either layout (ld == 0: packed).
+// RoPE sin / cos of rotation pair fi at position pos (half = rope dims):
+// modules.py:73-81: fp32 inverse frequency (10000 ** (2i / rope_dim))^-1,
+// fp32 angle pos * inv, sin / cos rounded to the activation dtype.
+CADENCE_DEV void rope_sincos(int pos, int fi, int half, float& sn, float& cs) {
+  const float expo = (float)(2 * fi) / (float)half;
+  const float timescale = (float)pow(10000.0, (double)expo);
+  const float inv = 1.0f / timescale;
+  const float ang = (float)pos * inv;
+  sn = rbf((float)sin((double)ang));
+  cs = rbf((float)cos((double)ang));
+}
+
 CADENCE_DEV int64_t xoff(int m, int k, int64_t ld, int mt) {
   return ld ? (int64_t)m * ld + k : xpk(m, k, mt);
 }

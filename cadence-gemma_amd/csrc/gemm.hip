@@ -197,6 +197,57 @@ struct EpiLinearConv : EpiLinear {
   }
 };
 
+// Decode q|k|v projection with RoPE in the epilogue (stream engine, M <= 32).
+// The weight rows are pre-permuted so that each rotation pair (dims i and
+// i + hd/4 of the rotated half of a q or k head) sits in adjacent columns
+// 2i, 2i + 1: the two values of a pair are in neighbouring lanes of one
+// wave (apply_pair gets the partner by a lane swap).  Columns hd/2.. of a
+// head and the v head are unpermuted.  Output rows go to q [M][H*hd],
+// k [M][hd], v [M][hd] in the natural dim order, with rope_qkv_kernel's
+// products, sums and roundings (modules.py:73-81 via attention.hip).
+struct EpiRopeQKV {
+  static constexpr bool kPaired = false;
+  static constexpr bool kStaged = false;
+  static constexpr bool kTile = false;
+  static constexpr bool kPairLanes = true;
+  u16* q; u16* k; u16* v;
+  const int32_t* pos;
+  const u16* table; int table_len;
+  int H, hd;
+  CADENCE_DEV float value(int64_t, int, float x, int) const { return rbf(x); }
+  CADENCE_DEV void apply_pair(int64_t m, int n, float x, float y) const {
+    const int h = n / hd, d = n % hd;
+    const int half = hd / 2, quarter = hd / 4;
+    u16* dst = h < H ? q + m * (int64_t)H * hd + (int64_t)h * hd
+                     : (h == H ? k + m * hd : v + m * hd);
+    if (h > H || d >= half) {            // v head / pass-through dims
+      dst[d] = f2bf(x);
+      return;
+    }
+    const int i = d >> 1;                 // rotation pair
+    const int p = pos[m];
+    float sn, cs;
+    if (p >= 0 && p < table_len) {
+      sn = bf2f(table[((int64_t)p * 2) * quarter + i]);
+      cs = bf2f(table[((int64_t)p * 2 + 1) * quarter + i]);
+    } else {
+      rope_sincos(p, i, half, sn, cs);
+    }
+    if ((d & 1) == 0)                     // x = dim i, y = dim i + hd/4
+      dst[i] = f2bf(bsub(bmul(x, cs), bmul(y, sn)));
+    else                                  // x = dim i + hd/4, y = dim i
+      dst[i + quarter] = f2bf(badd(bmul(x, cs), bmul(y, sn)));
+  }
+  CADENCE_DEV void apply(int64_t, int, float, int) const {}
+};
+
+template <class E, class = void>
+struct EpiPairLanes { static constexpr bool value = false; };
+template <class E>
+struct EpiPairLanes<E, std::void_t<decltype(E::kPairLanes)>> {
+  static constexpr bool value = E::kPairLanes;
+};
+
 // Epilogues that load per-element operands at kernel start (kPrefetch).
 template <class E, class = void>
 struct EpiPrefetch { static constexpr bool value = false; };
@@ -1038,6 +1089,14 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
     } else if constexpr (Epi::kPaired) {
       const int grp = blockIdx.x >> 1, half = blockIdx.x & 1;
       epi.apply2(m, grp * 32 + half * 16 + c, v[0], v[NREP - 1], g);
+    } else if constexpr (EpiPairLanes<Epi>::value) {
+      // lanes o and o ^ 1 hold the two columns of a pair (same row m)
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        const float x = epi.value(m, col[j] + c, v[j], g);
+        const float y = __shfl_xor(x, 1, 64);
+        epi.apply_pair(m, col[j] + c, x, y);
+      }
     } else if constexpr (kPf) {
 #pragma unroll
       for (int j = 0; j < NREP; ++j) epi.apply_pf(m, col[j] + c, v[j], g, pf[j]);
@@ -1641,6 +1700,26 @@ int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
     case 3: run(std::integral_constant<int, 3>{}); break;
     default: run(std::integral_constant<int, 4>{}); break;
   }
+  return (int)hipGetLastError();
+}
+
+int cadence_qkv_rope_decode(const void* A, int64_t lda, const void* Wperm,
+                            int64_t ldw, const int32_t* positions, void* q_out,
+                            void* k_out, void* v_out, int64_t M, int64_t H,
+                            int64_t hd, int64_t K, const void* table,
+                            int64_t table_len, void* stream) {
+  if (M <= 0) return 0;
+  const int64_t N = (H + 2) * hd;
+  int ksw = 0, ss = 0;
+  if (M > 32 || hd % 64 || H < 1 || K % 32 || (ldw != 0 && ldw < K) ||
+      (lda != 0 && lda < K) || !positions || !stream_plan(M, K, &ksw, &ss) || ss != 1)
+    return (int)hipErrorInvalidValue;
+  EpiRopeQKV epi{static_cast<u16*>(q_out), static_cast<u16*>(k_out),
+                 static_cast<u16*>(v_out), positions, static_cast<const u16*>(table),
+                 table ? (int)table_len : 0, (int)H, (int)hd};
+  launch_stream(static_cast<const u16*>(A), lda, static_cast<const u16*>(Wperm), ldw,
+                M, N, K, 1, 0, 0, epi, ksw, 1, nullptr, ldw == 0 ? 1 : 0,
+                static_cast<hipStream_t>(stream));
   return (int)hipGetLastError();
 }
 

@@ -256,6 +256,21 @@ int cadence_rope_qkv(const void* qkv, int64_t ldqkv, const int32_t* positions,
                      int64_t H, int64_t hd, const void* table,
                      int64_t table_len, void* stream);
 
+/* Decode (M <= 32 sequences, one token each) q|k|v projection with RoPE in
+ * the epilogue (replaces cadence_gemm_linear + cadence_rope_qkv for the
+ * cached attention step; reference modules.py:429-440 proj_q/k/v + apply_rope):
+ * Wperm is the [(H + 2) * hd][K] matrix [proj_q; proj_k; proj_v] with, in each
+ * of the H + 1 q / k heads, row 2i holding dim i and row 2i + 1 dim i + hd/4
+ * for i < hd/4 (the rotated half's pairs side by side; rows hd/2.. and the
+ * v head in natural order).  Outputs q [M][H*hd], k [M][hd], v [M][hd] as
+ * cadence_rope_qkv writes them.  Wperm may be fragment-packed (ldw == 0), A
+ * packed rows (lda == 0); K <= 2560 (one split). */
+int cadence_qkv_rope_decode(const void* A, int64_t lda, const void* Wperm,
+                            int64_t ldw, const int32_t* positions, void* q_out,
+                            void* k_out, void* v_out, int64_t M, int64_t H,
+                            int64_t hd, int64_t K, const void* table,
+                            int64_t table_len, void* stream);
+
 /* sin / cos table for cadence_rope_qkv: table[p][0][i] = bf16(sin(p * f_i)),
  * table[p][1][i] = bf16(cos(p * f_i)), i < hd / 4, f_i as modules.py:73-77
  * computes it (fp32 inverse frequencies, fp32 angle).  Positions >= the

@@ -46,3 +46,25 @@ def test_linear_conv1d_rejects_prefill_rows(dev):
   st = torch.zeros(40, 3, e, dtype=BF, device=dev)
   with pytest.raises(RuntimeError):
     ops.ops.gemm_linear_conv1d_(x, w, None, cw, cb, st)
+
+
+@pytest.mark.parametrize("m,packed", [(32, True), (9, False)])
+def test_qkv_rope_decode_matches_linear_then_rope(dev, m, packed):
+  """cadence_qkv_rope_decode (permuted weight, RoPE in the epilogue) ==
+  cadence_gemm_linear + cadence_rope_qkv, bit for bit, incl. positions
+  outside the sin/cos table (computed on the fly) and negative positions."""
+  g = torch.Generator().manual_seed(33)
+  h, hd, k = 10, 256, 2560
+  x = rnd(m, k, gen=g).to(dev)
+  w = rnd((h + 2) * hd, k, scale=k ** -0.5, gen=g).to(dev)
+  pos = torch.randint(0, 3000, (m,), generator=g, dtype=torch.int32)
+  pos[0] = 5000                      # past the table
+  pos[-1] = -1                       # padding position
+  pos = pos.to(dev)
+  table = ops.rope_table(dev, hd)
+  a = ops.pack_rows(x) if packed else x
+  qkv = ops.linear(a, w)
+  q1, k1, v1 = ops.ops.rope_qkv(qkv, pos, h, hd, table)
+  wp = w[ops.qkv_rope_permutation(h, hd, dev)].contiguous()
+  q2, k2, v2 = ops.qkv_rope_decode(a, wp, pos, h, hd)
+  assert torch.equal(q1, q2) and torch.equal(k1, k2) and torch.equal(v1, v2)
