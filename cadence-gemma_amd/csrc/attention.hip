@@ -765,7 +765,13 @@ int cadence_local_attention_decode(const void* q, const void* k_new,
                (int)window, 1.0f / sqrtf((float)hd),
                static_cast<float*>(workspace), sems};
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const dim3 grid((unsigned)B, split ? kDecodeSplits : 1);
+  // window splits per sequence (CADENCE_DECODE_ATTN_SPLITS, 1..8, for A/B)
+  static const int nsplit = [] {
+    const char* e = getenv("CADENCE_DECODE_ATTN_SPLITS");
+    const int v = e ? atoi(e) : kDecodeSplits;
+    return v >= 1 && v <= kDecodeSplits ? v : kDecodeSplits;
+  }();
+  const dim3 grid((unsigned)B, split ? nsplit : 1);
   if (hd == 256)
     hipLaunchKernelGGL(decode_attn_kernel<256>, grid, dim3(256), 0, st, a);
   else if (hd == 128)
