@@ -94,6 +94,23 @@ def make_inputs(global_batch, lo, hi, image_size, prompt, vocab, text_only):
   return tok[lo:hi].contiguous(), images
 
 
+def pmc_traffic(key):
+  """Per-launch HBM bytes of `key` from the newest committed PMC summary
+  (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.sh from
+  rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+  import glob
+  files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+  for f in reversed(files):
+    try:
+      with open(f) as fh:
+        k = json.load(fh).get("kernels", {}).get(key)
+    except (OSError, ValueError):
+      continue
+    if k and k.get("hbm_bytes_per_launch"):
+      return float(k["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
+  return None
+
+
 def roofline_entry(summary, key, bound):
   s = summary.get(key)
   if not s or s["avg_ms"] <= 0:
@@ -104,9 +121,13 @@ def roofline_entry(summary, key, bound):
   else:
     achieved = s["avg_work"] / (s["avg_ms"] * 1e-3) / 1e12
     peak, unit = MFMA_BF16_PEAK_TFS, "TFLOP/s"
+  tr = pmc_traffic(key)
   return {"kernel": key, "bound": bound, "achieved": round(achieved, 2),
           "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
-          "traffic": None, "avg_us": round(s["avg_ms"] * 1e3, 2),
+          "traffic": round(tr[0]) if tr else None,
+          "traffic_source": (f"{tr[1]}: bytes/launch, 2*FETCH_SIZE + WRITE_SIZE "
+                             "(fabric-side, Infinity-Cache hits included)") if tr else None,
+          "avg_us": round(s["avg_ms"] * 1e3, 2),
           "launches_timed": s["launches"],
           "work_per_launch": s["avg_work"]}
 
