@@ -84,6 +84,62 @@ __global__ __launch_bounds__(256) void rmsnorm_wide_kernel(
 }
 
 // timm LayerNorm (eps 1e-6) over the fp32 residual stream, bf16 out.
+// Rows up to 256 * RC wide (ViT widths 1024, 1152): the row is loaded once
+// into registers, with w / b, all before the first reduction (one memory
+// round trip instead of three); the sums keep layernorm_kernel's order, so
+// the results are identical.
+template <int RC>
+__global__ __launch_bounds__(256) void layernorm_reg_kernel(
+    const float* __restrict__ x, int64_t ldx, const u16* __restrict__ w,
+    const u16* __restrict__ b, u16* __restrict__ out, int64_t ldo,
+    int64_t rows, int width, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * ldx;
+  float4 v[RC];
+  uint2 wq[RC], bq[RC];
+#pragma unroll
+  for (int i = 0; i < RC; ++i) {
+    const int c = min(lane * 4 + i * 256, width - 4);
+    v[i] = *reinterpret_cast<const float4*>(xr + c);
+    wq[i] = *reinterpret_cast<const uint2*>(w + c);
+    bq[i] = *reinterpret_cast<const uint2*>(b + c);
+  }
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < RC; ++i)
+    if (lane * 4 + i * 256 < width) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  const float mean = wave_sum(s) / (float)width;
+  float q = 0.0f;
+#pragma unroll
+  for (int i = 0; i < RC; ++i)
+    if (lane * 4 + i * 256 < width) {
+      const float d0 = v[i].x - mean, d1 = v[i].y - mean, d2 = v[i].z - mean,
+                  d3 = v[i].w - mean;
+      q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)width + eps);
+  u16* orow = out + row * ldo;
+#pragma unroll
+  for (int i = 0; i < RC; ++i) {
+    const int c = lane * 4 + i * 256;
+    if (c >= width) continue;
+    const float vv[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+    const uint32_t wv[2] = {wq[i].x, wq[i].y}, bv[2] = {bq[i].x, bq[i].y};
+    uint32_t o[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float w0 = __uint_as_float(wv[j] << 16), w1 = __uint_as_float(wv[j] & 0xffff0000u);
+      const float b0 = __uint_as_float(bv[j] << 16), b1 = __uint_as_float(bv[j] & 0xffff0000u);
+      const float y0 = (vv[2 * j] - mean) * rstd * w0 + b0;
+      const float y1 = (vv[2 * j + 1] - mean) * rstd * w1 + b1;
+      o[j] = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
+    }
+    *reinterpret_cast<uint2*>(orow + c) = make_uint2(o[0], o[1]);
+  }
+}
+
 __global__ __launch_bounds__(256) void layernorm_kernel(
     const float* __restrict__ x, int64_t ldx, const u16* __restrict__ w,
     const u16* __restrict__ b, u16* __restrict__ out, int64_t ldo,
@@ -235,11 +291,17 @@ int cadence_layernorm(const float* x, int64_t ldx, const void* weight,
                       int64_t width, float eps, void* stream) {
   if (width % 4 || ldx % 4 || ldo % 4) return (int)hipErrorInvalidValue;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((rows + 3) / 4)),
-                     dim3(256), 0, static_cast<hipStream_t>(stream), x, ldx,
-                     static_cast<const u16*>(weight),
-                     static_cast<const u16*>(bias), static_cast<u16*>(out), ldo,
-                     rows, (int)width, eps);
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const u16* wp = static_cast<const u16*>(weight);
+  const u16* bp = static_cast<const u16*>(bias);
+  u16* op = static_cast<u16*>(out);
+  if (width <= 1280)
+    hipLaunchKernelGGL(layernorm_reg_kernel<5>, grid, block, 0, st, x, ldx, wp, bp, op,
+                       ldo, rows, (int)width, eps);
+  else
+    hipLaunchKernelGGL(layernorm_kernel, grid, block, 0, st, x, ldx, wp, bp, op, ldo,
+                       rows, (int)width, eps);
   return (int)hipGetLastError();
 }
 
