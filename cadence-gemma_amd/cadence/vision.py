@@ -178,6 +178,13 @@ class VisionTransformer(nn.Module):
                     col_off: int, blocks_run: int):
     """Runs the encoder on [B,3,S,S] pixels in [0,1]; writes bf16 features of
     block `blocks_run - 1` (prefix dropped) to out2d[:, col_off:col_off+D]."""
+    for _ in self.feature_steps(pixels, out2d, col_off, blocks_run):
+      pass
+
+  def feature_steps(self, pixels: torch.Tensor, out2d: torch.Tensor,
+                    col_off: int, blocks_run: int):
+    """features_into as a generator: one yield after each enqueued block, so
+    a caller can interleave the launches of two encoders on two streams."""
     cfg = self.cfg
     b = pixels.shape[0]
     assert pixels.shape[-1] == self.image_size, "image size mismatch"
@@ -195,6 +202,7 @@ class VisionTransformer(nn.Module):
     r2 = resid.view(b * ntok, cfg.width)
     for i in range(blocks_run):
       self.blocks[i].run(r2, b, ntok)
+      yield i
     ops.ops.vit_features_(resid, out2d, col_off, b, ntok, npre)
 
 
@@ -242,12 +250,21 @@ class VisionEncoder(nn.Module):
     cur = torch.cuda.current_stream(pixels.device)
     side = self._side_stream(pixels.device)
     side.wait_stream(cur)
+    # the two towers' launches are interleaved block by block, so both
+    # streams have work queued from the start (enqueueing one whole tower
+    # first leaves the other stream idle for the host time that takes)
+    dino = self.dino.feature_steps(pixels, out2d, 0, n)
+    sig = self.siglip.feature_steps(pixels, out2d, self.config.dino.width, n)
     with ops.TIMER.scoped(" [vit, 2 streams]"):
-      with torch.cuda.stream(side):
-        self.siglip.features_into(pixels, out2d, self.config.dino.width, n)
+      live = [True, True]
+      while any(live):
+        if live[1]:
+          with torch.cuda.stream(side):
+            live[1] = next(sig, None) is not None
+        if live[0]:
+          live[0] = next(dino, None) is not None
       pixels.record_stream(side)
       out2d.record_stream(side)
-      self.dino.features_into(pixels, out2d, 0, n)
     cur.wait_stream(side)
 
   def encode(self, pixels: torch.Tensor) -> torch.Tensor:
