@@ -23,6 +23,36 @@
 
 namespace {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// max without the IEEE sNaN-quieting v_max the fmaxf lowering adds (scores
+// are finite or -inf)
+CADENCE_DEV float max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+CADENCE_DEV float max2(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// max over lanes l, l ^ 16, l ^ 32, l ^ 48 (the four 16-lane rows) with the
+// gfx950 row swaps instead of two LDS-routed ds_bpermute
+CADENCE_DEV float max_rows(float v) {
+  const uint32_t u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  const float m = max2(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const uint32_t w = __float_as_uint(m);
+  const auto b = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return max2(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+// two fp32 -> packed bf16 pair in one v_cvt_pk_bf16_f32 (RNE)
+CADENCE_DEV uint32_t pk2bf(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+
 // V^T columns are stored in the P^T slot order of each 32-key group (slot
 // 8g + j <-> key 4g + j for j < 4, 16 + 4g + j - 4 for j >= 4), so a lane's 8
 // keys of a PV k-step are one 16-B run.  vslot(k) for a key k = 4q.
@@ -195,15 +225,19 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
             for (int r = 0; r < 4; ++r)
               if (c0 + 16 * t + 4 * g + r >= N) s[u][t][r] = -INFINITY;
         }
-        float smax = fmaxf(fmaxf(s[u][0][0], s[u][0][1]), fmaxf(s[u][0][2], s[u][0][3]));
-#pragma unroll
-        for (int t = 1; t < 4; ++t) {
-          if (t >= 2 && two) continue;
-          smax = fmaxf(smax, fmaxf(fmaxf(s[u][t][0], s[u][t][1]),
-                                   fmaxf(s[u][t][2], s[u][t][3])));
+        float smax = max3(s[u][0][0], s[u][0][1], s[u][0][2]);
+        smax = max3(smax, s[u][0][3], s[u][1][0]);
+        smax = max3(smax, s[u][1][1], s[u][1][2]);
+        if (two) {
+          smax = max2(smax, s[u][1][3]);
+        } else {
+          smax = max3(smax, s[u][1][3], s[u][2][0]);
+          smax = max3(smax, s[u][2][1], s[u][2][2]);
+          smax = max3(smax, s[u][2][3], s[u][3][0]);
+          smax = max3(smax, s[u][3][1], s[u][3][2]);
+          smax = max2(smax, s[u][3][3]);
         }
-        smax = fmaxf(smax, __shfl_xor(smax, 16, 64));
-        smax = fmaxf(smax, __shfl_xor(smax, 32, 64));
+        smax = max_rows(smax);
         const float mt = smax * scale_log2;
         const bool need = mt > m[u] + kThr;
         if (__any(need)) {
@@ -217,7 +251,7 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
           m[u] = mn;
         }
         const float nm = -m[u];
-        float ps = 0.0f;
+        float ps0 = 0.0f, ps1 = 0.0f;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           uint32_t pk[4] = {0u, 0u, 0u, 0u};
@@ -227,13 +261,14 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
               const int t = 2 * kk + (j >> 2), r = j & 3;
               const float e0 = __builtin_amdgcn_exp2f(fmaf(s[u][t][r], scale_log2, nm));
               const float e1 = __builtin_amdgcn_exp2f(fmaf(s[u][t][r + 1], scale_log2, nm));
-              ps += e0 + e1;
-              pk[j >> 1] = (uint32_t)f2bf(e0) | ((uint32_t)f2bf(e1) << 16);
+              ps0 += e0;
+              ps1 += e1;
+              pk[j >> 1] = pk2bf(f32x2{e0, e1});   // one cvt for the pair
             }
           }
           pf[u][kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
         }
-        l[u] += ps;
+        l[u] += ps0 + ps1;
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -313,7 +348,6 @@ __attribute__((visibility("hidden"))) int vit_attention_lds_launch(
 #define VSEL(HDK_, HDV_, NP_, KW_, VR_, DEF)                                          \
   switch (cfg ? cfg : DEF) {                                                          \
     case 81: VA(HDK_, HDV_, NP_, 8, 1, KW_, VR_); break;                              \
-    case 82: VA(HDK_, HDV_, NP_, 8, 2, KW_, VR_); break;                              \
     default: return -1;                                                               \
   }
   // 8 waves x 1 query tile (DINO's 17 tiles on 9 waves measured 10 % slower:
