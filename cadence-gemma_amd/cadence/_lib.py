@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -72,6 +72,7 @@ _SIGS: dict[str, list] = {
     "cadence_vit_prefix": [P, P, I64, I64, I64, I64, P],
     "cadence_vit_attention": [P, P, I64, I64, I64, I64, P],
     "cadence_vit_features": [P, P, I64, I64, I64, I64, I64, I64, P],
+    "cadence_resize_bicubic": [P, P, I64, I64, I64, I64, P, P, P, P],
     "cadence_splice_positions": [P, P, I64, I64, I64, P],
     "cadence_decode_advance": [P, P, I64, P, P, P, I64, P],
 }

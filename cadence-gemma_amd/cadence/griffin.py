@@ -78,8 +78,12 @@ class Griffin(nn.Module):
     if images is not None:
       return images.to(dev, torch.float32).contiguous()
     from . import image_io
-    px = image_io.load_image(img_path, self.vision_config.image_size)
-    return px[None].expand(batch, -1, -1, -1).contiguous().to(dev)
+    px = image_io.load_images(img_path, self.vision_config.image_size, dev)
+    if px.shape[0] == batch:        # a list of B paths: one image per sample
+      return px
+    if px.shape[0] != 1:
+      raise ValueError(f"{px.shape[0]} images for a batch of {batch}")
+    return px.expand(batch, -1, -1, -1).contiguous()   # reference: one image
 
   def embed_inputs(self, tokens, segment_pos, images=None, img_path=None):
     """Returns (x [B*L, D], positions [B, L] int32, L) with the image spliced."""
@@ -130,7 +134,7 @@ class Griffin(nn.Module):
   @torch.no_grad()
   def forward(self, tokens: torch.Tensor, segment_pos: torch.Tensor,
               cache: Cache | None = None, return_logits: bool = True,
-              return_cache: bool = True, img_path: str | None = None,
+              return_cache: bool = True, img_path: str | list[str] | None = None,
               images: torch.Tensor | None = None):
     if not return_logits and not return_cache:
       return None, None

@@ -14,6 +14,7 @@ what the modules call; they route through `torch.ops.cadence`.
 from __future__ import annotations
 
 import contextlib
+import math
 import os
 from typing import NamedTuple
 
@@ -788,6 +789,30 @@ def _im2col(pixels, mean, std, patch, kpad):
   _lib.check(_lib.load().cadence_im2col_normalize(
       _p(pixels), _p(out), kpad, B, S, patch, ctypes.cast(m3, ctypes.c_void_p),
       ctypes.cast(s3, ctypes.c_void_p), _s(pixels)), "im2col")
+  return out
+
+
+def resize_taps(in_size: int, size: int) -> int:
+  """Pillow precompute_coeffs ksize for one image side (Resample.c):
+  ceil(2 * max(in / S, 1)) * 2 + 1, in the same double arithmetic."""
+  scale = float(in_size) / size
+  return int(math.ceil(2.0 * max(scale, 1.0))) * 2 + 1
+
+
+@_reg("resize_bicubic(Tensor images, Tensor meta, int S, int KS, int max_h, "
+      "int tmp_bytes) -> Tensor")
+def _resize_bicubic(images, meta, S, KS, max_h, tmp_bytes):
+  _need(images.dtype == torch.uint8 and images.dim() == 1, "images packed u8")
+  _need(meta.dtype == torch.int64 and meta.dim() == 2 and meta.shape[1] == 4
+        and meta.is_contiguous() and meta.device == images.device,
+        "meta [B, 4] int64 on the images' device")
+  B = meta.shape[0]
+  out = torch.empty(B, 3, S, S, dtype=_F32, device=images.device)
+  coef = torch.empty(B * 2 * S * (2 + KS), dtype=_I32, device=images.device)
+  tmp = torch.empty(max(tmp_bytes, 1), dtype=torch.uint8, device=images.device)
+  _lib.check(_lib.load().cadence_resize_bicubic(
+      _p(images), _p(meta), B, S, KS, max_h, _p(coef), _p(tmp), _p(out),
+      _s(images)), "resize_bicubic")
   return out
 
 

@@ -275,11 +275,12 @@ class VisionEncoder(nn.Module):
     return out.view(b, self.n_visual_tokens, -1)
 
   def forward(self, img_path_or_pixels) -> torch.Tensor:
-    """`forward(img_path)` (reference API) or `forward(pixels [B,3,S,S])`."""
-    if isinstance(img_path_or_pixels, str):
+    """`forward(img_path)` (reference API), a list of paths (one image per
+    sample, resized on the GPU), or `forward(pixels [B,3,S,S])`."""
+    if isinstance(img_path_or_pixels, (str, list, tuple)):
       from . import image_io
-      pixels = image_io.load_image(img_path_or_pixels, self.config.image_size)
-      pixels = pixels[None].to(self.device)
+      pixels = image_io.load_images(img_path_or_pixels, self.config.image_size,
+                                    self.device)
     else:
       pixels = img_path_or_pixels
     return self.encode(pixels)

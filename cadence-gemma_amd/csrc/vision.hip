@@ -66,6 +66,112 @@ __global__ __launch_bounds__(256) void features_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Image preprocessing: Resize((S, S), BICUBIC) of torchvision on a PIL image
+// (dino_siglip.py:12-16, 88-124, 148-151) is Pillow's ImagingResample
+// (libImaging/Resample.c; Pillow is a third-party dependency, restated here):
+//   * per output index i: center = (i + 0.5) * scale, scale = in / S,
+//     filterscale = max(scale, 1), support = 2 * filterscale,
+//     taps [xmin, xmin + n) with xmin = (int)(center - support + 0.5) >= 0,
+//     xmax = min((int)(center + support + 0.5), in); weights
+//     w = cubic((x + xmin - center + 0.5) / filterscale), a = -0.5,
+//     normalised by their double sum, then fixed point:
+//     k = (int)(w * 2^22 +- 0.5) (PRECISION_BITS = 32 - 8 - 2)
+//   * horizontal pass first into a uint8 image [H, S, 3], then the vertical
+//     pass; each output = clamp((2^21 + sum u8 * k) >> 22, 0, 255)
+//   * ToTensor: u8 / 255 in fp32; CenterCrop(S) after a square resize is a
+//     no-op.
+// The coefficient tables are built on the device in IEEE double (no FMA
+// contraction: -ffp-contract=off), exactly as Pillow builds them on the host.
+// Ragged batch: meta[b] = {byte offset of image b in `images` (packed HWC
+// RGB), H, W, byte offset of its [H, S, 3] row-pass image in tmp}.
+
+__device__ __forceinline__ double pil_bicubic(double x) {
+  const double a = -0.5;
+  if (x < 0.0) x = -x;
+  if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+  if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+  return 0.0;
+}
+
+// One thread per (image, axis, output index).  Table of image b, axis ax:
+// bounds at coef + ((b * 2 + ax) * S) * (2 + KS), row i = {xmin, n, k[KS]}.
+__global__ __launch_bounds__(256) void resize_coeff_kernel(
+    const int64_t* __restrict__ meta, int32_t* __restrict__ coef, int S,
+    int KS) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int ax = blockIdx.y, b = blockIdx.z;
+  if (i >= S) return;
+  const int in_size = (int)meta[b * 4 + 1 + (ax == 0 ? 1 : 0)];  // ax 0: W, 1: H
+  int32_t* row = coef + ((int64_t)(b * 2 + ax) * S + i) * (2 + KS);
+  const double scale = (double)(float)in_size / S;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 2.0 * filterscale;
+  const double center = (i + 0.5) * scale;
+  const double ss = 1.0 / filterscale;
+  int xmin = (int)(center - support + 0.5);
+  if (xmin < 0) xmin = 0;
+  int xmax = (int)(center + support + 0.5);
+  if (xmax > in_size) xmax = in_size;
+  xmax -= xmin;
+  double ww = 0.0;
+  for (int x = 0; x < xmax; ++x) ww += pil_bicubic((x + xmin - center + 0.5) * ss);
+  row[0] = xmin;
+  row[1] = xmax < KS ? xmax : KS;   // host sizes KS >= every n
+  for (int x = 0; x < KS; ++x) {
+    double w = 0.0;
+    if (x < xmax) {
+      w = pil_bicubic((x + xmin - center + 0.5) * ss);
+      if (ww != 0.0) w /= ww;
+    }
+    const double f = w * (double)(1 << 22);
+    row[2 + x] = w < 0 ? (int32_t)(-0.5 + f) : (int32_t)(0.5 + f);
+  }
+}
+
+__device__ __forceinline__ uint8_t pil_clip8(int32_t ss) {
+  const int32_t v = ss >> 22;
+  return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+// Row pass: block (row y, image b); threads over the S * 3 outputs of the row.
+__global__ __launch_bounds__(256) void resize_rows_kernel(
+    const uint8_t* __restrict__ images, const int64_t* __restrict__ meta,
+    const int32_t* __restrict__ coef, uint8_t* __restrict__ tmp, int S, int KS) {
+  const int y = blockIdx.x, b = blockIdx.y;
+  const int H = (int)meta[b * 4 + 1], W = (int)meta[b * 4 + 2];
+  if (y >= H) return;
+  const uint8_t* src = images + meta[b * 4 + 0] + (int64_t)y * W * 3;
+  uint8_t* dst = tmp + meta[b * 4 + 3] + (int64_t)y * S * 3;
+  const int32_t* tab = coef + (int64_t)(b * 2 + 0) * S * (2 + KS);
+  for (int o = threadIdx.x; o < S * 3; o += 256) {
+    const int xx = o / 3, c = o - xx * 3;
+    const int32_t* row = tab + (int64_t)xx * (2 + KS);
+    const int xmin = row[0], n = row[1];
+    int32_t acc = 1 << 21;
+    for (int x = 0; x < n; ++x) acc += (int32_t)src[(xmin + x) * 3 + c] * row[2 + x];
+    dst[o] = pil_clip8(acc);
+  }
+}
+
+// Column pass + ToTensor: block (output row yy, image b); threads over
+// (c, xx) so each channel plane row is written contiguously.
+__global__ __launch_bounds__(256) void resize_cols_kernel(
+    const uint8_t* __restrict__ tmp, const int64_t* __restrict__ meta,
+    const int32_t* __restrict__ coef, float* __restrict__ out, int S, int KS) {
+  const int yy = blockIdx.x, b = blockIdx.y;
+  const uint8_t* src = tmp + meta[b * 4 + 3];
+  const int32_t* row = coef + ((int64_t)(b * 2 + 1) * S + yy) * (2 + KS);
+  const int ymin = row[0], n = row[1];
+  for (int o = threadIdx.x; o < S * 3; o += 256) {
+    const int c = o / S, xx = o - c * S;
+    int32_t acc = 1 << 21;
+    for (int y = 0; y < n; ++y)
+      acc += (int32_t)src[((int64_t)(ymin + y) * S + xx) * 3 + c] * row[2 + y];
+    out[(((int64_t)b * 3 + c) * S + yy) * S + xx] = (float)pil_clip8(acc) / 255.0f;
+  }
+}
+
 int grid_cap(int64_t work) {
   int64_t g = (work + 255) / 256;
   if (g < 1) g = 1;
@@ -111,6 +217,24 @@ int cadence_vit_features(const float* resid, void* out, int64_t ldo,
                      static_cast<hipStream_t>(stream), resid,
                      static_cast<u16*>(out), ldo, col_off, (int)B, (int)ntok,
                      (int)prefix, (int)D);
+  return (int)hipGetLastError();
+}
+
+int cadence_resize_bicubic(const void* images, const int64_t* meta, int64_t B,
+                           int64_t S, int64_t KS, int64_t max_h, void* coef,
+                           void* tmp, float* out, void* stream) {
+  if (B <= 0) return 0;
+  if (S <= 0 || KS < 5 || max_h <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int32_t* tab = static_cast<int32_t*>(coef);
+  hipLaunchKernelGGL(resize_coeff_kernel, dim3((S + 255) / 256, 2, B), dim3(256),
+                     0, s, meta, tab, (int)S, (int)KS);
+  hipLaunchKernelGGL(resize_rows_kernel, dim3(max_h, B), dim3(256), 0, s,
+                     static_cast<const uint8_t*>(images), meta, tab,
+                     static_cast<uint8_t*>(tmp), (int)S, (int)KS);
+  hipLaunchKernelGGL(resize_cols_kernel, dim3(S, B), dim3(256), 0, s,
+                     static_cast<const uint8_t*>(tmp), meta, tab, out, (int)S,
+                     (int)KS);
   return (int)hipGetLastError();
 }
 

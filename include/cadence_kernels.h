@@ -336,6 +336,21 @@ int cadence_vit_features(const float* resid, void* out, int64_t ldo,
                          int64_t col_off, int64_t B, int64_t ntok,
                          int64_t prefix, int64_t D, void* stream);
 
+/* Image preprocessing of the img_path API: torchvision Resize((S, S),
+ * BICUBIC) on a PIL RGB image + ToTensor (dino_siglip.py:12-16, 88-124,
+ * 148-151; both encoders' transforms share it), i.e. Pillow's
+ * ImagingResample (libImaging/Resample.c) bit for bit, for a ragged batch:
+ *   images  packed uint8 HWC RGB; meta[b] = {byte offset, H, W, tmp offset}
+ *   KS      taps per coefficient row >= 2 * ceil(2 * max(in / S, 1)) + 1 over
+ *           every image side (host computes it)
+ *   coef    workspace, B * 2 * S * (2 + KS) int32
+ *   tmp     workspace, sum_b H_b * S * 3 bytes (the row-pass images)
+ *   out     [B, 3, S, S] fp32 in [0, 1]
+ * Replaces the host PIL resize per image in VisionEncoder.forward. */
+int cadence_resize_bicubic(const void* images, const int64_t* meta, int64_t B,
+                           int64_t S, int64_t KS, int64_t max_h, void* coef,
+                           void* tmp, float* out, void* stream);
+
 /* ---- misc ------------------------------------------------------------------ */
 
 /* Image splice positions (griffin.py:186-191, n_vis generalised):

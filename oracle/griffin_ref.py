@@ -329,6 +329,73 @@ def griffin_forward(p, cfg, tokens, segment_pos, cache=None, image_tokens=None,
   return logits, new_cache
 
 
+# ------------------------------------------------------ image preprocessing
+
+def pil_resize_to_tensor(rgb_u8, size):
+  """Resize((S, S), BICUBIC) + ToTensor exactly as the reference runs them
+  (dino_siglip.py:12-16, 88-124, 148-151: torchvision on a PIL image calls
+  `Image.resize(size, BICUBIC)`; ToTensor = permute + float / 255).  Pillow
+  itself is the checker here: [H, W, 3] uint8 -> [3, S, S] fp32."""
+  import numpy as np
+  from PIL import Image
+  img = Image.fromarray(np.ascontiguousarray(rgb_u8), "RGB")
+  img = img.resize((size, size), Image.BICUBIC)
+  return torch.from_numpy(np.array(img, dtype=np.uint8)).permute(
+      2, 0, 1).contiguous().to(torch.float32).div(255)
+
+
+def pil_resample_np(rgb_u8, size):
+  """Restatement of Pillow's ImagingResample (libImaging/Resample.c,
+  Pillow 12.x; third-party, not under /root/reference): precompute_coeffs
+  (bicubic a = -0.5, support 2 * max(scale, 1)), normalize_coeffs_8bpc
+  (22-bit fixed point), horizontal pass to uint8, then vertical pass.  The
+  HIP kernel follows this; tests pin it against Pillow itself."""
+  import numpy as np
+
+  def cubic(x):
+    a = -0.5
+    x = abs(x)
+    if x < 1.0:
+      return ((a + 2.0) * x - (a + 3.0)) * x * x + 1
+    if x < 2.0:
+      return (((x - 5) * x + 8) * x - 4) * a
+    return 0.0
+
+  def coeffs(in_size):
+    scale = float(in_size) / size
+    fs = max(scale, 1.0)
+    support = 2.0 * fs
+    ss = 1.0 / fs
+    rows = []
+    for i in range(size):
+      center = (i + 0.5) * scale
+      xmin = max(int(center - support + 0.5), 0)
+      xmax = min(int(center + support + 0.5), in_size) - xmin
+      w = [cubic((x + xmin - center + 0.5) * ss) for x in range(xmax)]
+      ww = sum(w)
+      w = [v / ww if ww != 0.0 else v for v in w]
+      k = [int(-0.5 + v * (1 << 22)) if v < 0 else int(0.5 + v * (1 << 22))
+           for v in w]
+      rows.append((xmin, np.array(k, dtype=np.int64)))
+    return rows
+
+  def clip8(acc):
+    return np.clip(acc >> 22, 0, 255).astype(np.uint8)
+
+  src = np.asarray(rgb_u8, dtype=np.int64)
+  h, w = src.shape[:2]
+  tmp = np.empty((h, size, 3), dtype=np.uint8)
+  for xx, (xmin, k) in enumerate(coeffs(w)):
+    acc = (1 << 21) + np.tensordot(k, src[:, xmin:xmin + len(k)], axes=([0], [1]))
+    tmp[:, xx] = clip8(acc)
+  tmp = tmp.astype(np.int64)
+  out = np.empty((size, size, 3), dtype=np.uint8)
+  for yy, (ymin, k) in enumerate(coeffs(h)):
+    acc = (1 << 21) + np.tensordot(k, tmp[ymin:ymin + len(k)], axes=([0], [0]))
+    out[yy] = clip8(acc)
+  return out
+
+
 # ------------------------------------------------ vision tower + projector
 
 def vit_features(pixels, p, prefix, vcfg, tower):

@@ -171,6 +171,27 @@ def mm_model():
           "mm.logits": logits, "mm.param_sums": sums}, keys
 
 
+IMAGES = ("car2.jpg", "german.jpg")   # recurrentgemma/vit/img_tests/ (data files)
+
+
+def images():
+  """pil_loader + Resize((S, S), BICUBIC) of two of the reference's own test
+  images (dino_siglip.py:12-16, 88-124), expected uint8 outputs from Pillow."""
+  import numpy as np
+  from PIL import Image
+  out = {}
+  for name in IMAGES:
+    with open(os.path.join(HERE, "images", name), "rb") as f:
+      img = Image.open(f).convert("RGB")
+    arr = np.asarray(img)
+    out[f"{name}.decoded_sum"] = torch.tensor([int(arr.astype(np.int64).sum())])
+    out[f"{name}.hw"] = torch.tensor(arr.shape[:2])
+    for size in (224, 336):
+      out[f"{name}.{size}"] = torch.from_numpy(
+          np.array(img.resize((size, size), Image.BICUBIC), dtype=np.uint8))
+  return out
+
+
 def main():
   torch.set_num_threads(min(8, os.cpu_count() or 1))
   save_file({k: v.contiguous() for k, v in kernels().items()},
@@ -183,6 +204,7 @@ def main():
   save_file({k: v.contiguous() for k, v in m.items()},
             os.path.join(HERE, "mm_model.safetensors"),
             metadata={"param_keys": ",".join(mkeys)})
+  save_file(images(), os.path.join(HERE, "images.safetensors"))
   for f in sorted(os.listdir(HERE)):
     if f.endswith(".safetensors"):
       print(f, os.path.getsize(os.path.join(HERE, f)))

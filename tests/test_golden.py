@@ -191,3 +191,40 @@ def test_golden_hip_multimodal(dev):
     got, _ = m(f["mm.tokens"].to(dev), f["mm.pos"].to(dev), images=px)
   assert got.shape == f["mm.logits"].shape
   assert cosine(got, f["mm.logits"]) > 0.999
+
+
+# ------------------------------------------------- image preprocessing
+
+def _decode(name):
+  from cadence import image_io
+  return image_io.decode_rgb(os.path.join(GOLD, "images", name))
+
+
+def test_golden_images_pillow_and_restatement():
+  """The reference's own test JPEGs: Pillow's bicubic resize (the
+  reference's transform) reproduces the fixture, and so does the oracle's
+  restatement of its resampler that the HIP kernel follows."""
+  f, _ = _load("images.safetensors")
+  for name in ("car2.jpg", "german.jpg"):
+    arr = _decode(name)
+    assert int(arr.astype("int64").sum()) == int(f[f"{name}.decoded_sum"][0])
+    for size in (224, 336):
+      want = f[f"{name}.{size}"]
+      got = R.pil_resize_to_tensor(arr, size)
+      assert torch.equal(got, want.permute(2, 0, 1).float().div(255))
+      if size == 224:
+        assert torch.equal(torch.from_numpy(R.pil_resample_np(arr, size)), want)
+
+
+@pytest.mark.gpu
+def test_golden_images_hip_resize(dev):
+  from cadence import image_io
+  f, _ = _load("images.safetensors")
+  names = ("car2.jpg", "german.jpg")
+  for size in (224, 336):
+    got = image_io.load_images([os.path.join(GOLD, "images", n) for n in names],
+                               size, dev).cpu()
+    assert got.shape == (2, 3, size, size)
+    for i, n in enumerate(names):
+      want = f[f"{n}.{size}"].permute(2, 0, 1).float().div(255)
+      assert torch.equal(got[i], want), (n, size)
