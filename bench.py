@@ -178,6 +178,48 @@ def vit_attention_isolated(vis, batch, dev, reps=20):
   return out
 
 
+def image_preprocess_isolated(batch, size, dev, reps=20, h=480, w=640):
+  """img_path preprocessing (Resize((S,S), BICUBIC) + ToTensor, Pillow-exact)
+  on `batch` synthetic h x w RGB uint8 images already resident in HBM, HIP
+  events around `reps` launches after the timed region; beside it Pillow's
+  host resize of the same images (the reference's transform, one core,
+  image by image as VisionEncoder.forward runs it)."""
+  import numpy as np
+  from PIL import Image
+  from cadence import image_io
+  rng = np.random.default_rng(99)
+  arrs = [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for _ in range(batch)]
+  meta = torch.tensor([[i * h * w * 3, h, w, i * h * size * 3] for i in range(batch)],
+                      dtype=torch.int64, device=dev)
+  packed = torch.from_numpy(np.concatenate([a.reshape(-1) for a in arrs])).to(dev)
+  ks = max(ops.resize_taps(h, size), ops.resize_taps(w, size))
+  run = lambda: torch.ops.cadence.resize_bicubic(packed, meta, size, ks, h, w,
+                                                 batch * h * size * 3)
+  run()
+  torch.cuda.synchronize()
+  s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+  s.record()
+  for _ in range(reps):
+    run()
+  e.record()
+  torch.cuda.synchronize()
+  us = s.elapsed_time(e) / reps * 1e3
+  nbytes = batch * (h * w * 3 + 3 * size * size * 4)     # u8 in + fp32 out
+  gbs = nbytes / (us * 1e-6) / 1e9
+  t0 = time.perf_counter()
+  for a in arrs[:8]:
+    Image.fromarray(a).resize((size, size), Image.BICUBIC)
+  host_s = (time.perf_counter() - t0) / 8
+  return {"kernel": "resize_coeff + resize_rows + resize_cols", "bound": "hbm",
+          "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+          "frac": round(gbs / HBM_PEAK_GBS, 4), "avg_us": round(us, 2),
+          "work_per_launch": nbytes, "images_per_s": round(batch / (us * 1e-6), 1),
+          "shape": f"B={batch} {h}x{w} -> {size}x{size}",
+          "cpu_pillow_images_per_s": round(1.0 / host_s, 1),
+          "timing": f"isolated, {reps} launches after the timed region; "
+                    "algorithmic bytes = u8 input + fp32 output"}
+
+
 def cpu_baseline(model, cfg, vis, tokens, images, decode_steps):
   """The oracle (reference op sequence, B = 1 like the reference) on host
   cores, on a bounded sample: 1 sample, full image + prompt prefill,
@@ -257,6 +299,8 @@ def main():
   ksum = ops.TIMER.summary() if not args.no_kernel_timing else {}
   vit_iso = (vit_attention_isolated(vis, args.batch, dev)
              if vis is not None and rank == 0 and not args.no_kernel_timing else None)
+  img_iso = (image_preprocess_isolated(args.batch, args.image_size, dev)
+             if vis is not None and rank == 0 and not args.no_kernel_timing else None)
 
   tok_per_step = gb * (n_vis + args.prompt + args.decode)
   value = tok_per_step * args.steps / elapsed
@@ -319,6 +363,7 @@ def main():
         "roofline_scan": roofline_entry(ksum, "rnn_scan_kernel", "hbm"),
         "roofline_decode": dec,
         "roofline_vit_attention": vit_iso,
+        "roofline_image_preprocess": img_iso,
         "roofline_by_kernel": {k: roofline_entry(ksum, k, "mfma") for k in sorted(ksum)
                                if k.startswith(("gemm_big", "vit_attn", "flash_attn"))},
         # a seeded 1/sample of the launches is event-timed (TIMER.sample)

@@ -72,7 +72,8 @@ _SIGS: dict[str, list] = {
     "cadence_vit_prefix": [P, P, I64, I64, I64, I64, P],
     "cadence_vit_attention": [P, P, I64, I64, I64, I64, P],
     "cadence_vit_features": [P, P, I64, I64, I64, I64, I64, I64, P],
-    "cadence_resize_bicubic": [P, P, I64, I64, I64, I64, P, P, P, P],
+    "cadence_resize_bicubic": [P, I64, P, I64, I64, I64, I64, I64, P, P, I64, P,
+                               P],
     "cadence_splice_positions": [P, P, I64, I64, I64, P],
     "cadence_decode_advance": [P, P, I64, P, P, P, I64, P],
 }

@@ -55,9 +55,9 @@ def resize_arrays(arrays: Sequence[np.ndarray], size: int,
     view[meta[i, 0]:meta[i, 0] + a.size] = np.ascontiguousarray(a).reshape(-1)
   dev_images = packed.to(device, non_blocking=True)
   dev_meta = torch.from_numpy(meta).pin_memory().to(device, non_blocking=True)
-  max_h = int(meta[:, 1].max())
+  max_h, max_w = int(meta[:, 1].max()), int(meta[:, 2].max())
   return torch.ops.cadence.resize_bicubic(dev_images, dev_meta, size, ks, max_h,
-                                          tmp)
+                                          max_w, tmp)
 
 
 def load_images(paths: str | Sequence[str], size: int, device,

@@ -792,6 +792,9 @@ def _im2col(pixels, mean, std, patch, kpad):
   return out
 
 
+RESIZE_MAX_ROW_BYTES = 32768 - 32   # one pixel row staged in LDS (vision.hip)
+
+
 def resize_taps(in_size: int, size: int) -> int:
   """Pillow precompute_coeffs ksize for one image side (Resample.c):
   ceil(2 * max(in / S, 1)) * 2 + 1, in the same double arithmetic."""
@@ -800,19 +803,23 @@ def resize_taps(in_size: int, size: int) -> int:
 
 
 @_reg("resize_bicubic(Tensor images, Tensor meta, int S, int KS, int max_h, "
-      "int tmp_bytes) -> Tensor")
-def _resize_bicubic(images, meta, S, KS, max_h, tmp_bytes):
-  _need(images.dtype == torch.uint8 and images.dim() == 1, "images packed u8")
+      "int max_w, int tmp_bytes) -> Tensor")
+def _resize_bicubic(images, meta, S, KS, max_h, max_w, tmp_bytes):
+  _need(images.dtype == torch.uint8 and images.dim() == 1
+        and images.is_contiguous(), "images packed u8")
   _need(meta.dtype == torch.int64 and meta.dim() == 2 and meta.shape[1] == 4
         and meta.is_contiguous() and meta.device == images.device,
         "meta [B, 4] int64 on the images' device")
+  _need(3 * max_w <= RESIZE_MAX_ROW_BYTES and 3 * S <= RESIZE_MAX_ROW_BYTES,
+        f"image width and S must be <= {RESIZE_MAX_ROW_BYTES // 3}")
   B = meta.shape[0]
+  KS = (KS + 3) // 4 * 4            # coefficient rows padded to whole fours
   out = torch.empty(B, 3, S, S, dtype=_F32, device=images.device)
   coef = torch.empty(B * 2 * S * (2 + KS), dtype=_I32, device=images.device)
   tmp = torch.empty(max(tmp_bytes, 1), dtype=torch.uint8, device=images.device)
   _lib.check(_lib.load().cadence_resize_bicubic(
-      _p(images), _p(meta), B, S, KS, max_h, _p(coef), _p(tmp), _p(out),
-      _s(images)), "resize_bicubic")
+      _p(images), images.numel(), _p(meta), B, S, KS, max_h, max_w, _p(coef),
+      _p(tmp), tmp.numel(), _p(out), _s(images)), "resize_bicubic")
   return out
 
 

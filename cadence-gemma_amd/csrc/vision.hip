@@ -134,41 +134,168 @@ __device__ __forceinline__ uint8_t pil_clip8(int32_t ss) {
   return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
-// Row pass: block (row y, image b); threads over the S * 3 outputs of the row.
+constexpr int kResizeRows = 8;          // input rows per row-pass block
+constexpr int kResizeOutRows = 8;       // output rows per column-pass block
+constexpr int kResizeLds = 32768;       // staged pixel bytes per block
+constexpr int kResizeCoefLds = 32768;   // coefficient table bytes (if it fits)
+constexpr int kResizeMaxKS = 126;       // column-pass coefficient rows in LDS
+
+// Loads bytes [start, start + len) of `src` (valid up to `nbytes`; `src`
+// 16-byte aligned) into LDS as aligned 16-byte quads, all of a thread's
+// loads issued before its LDS stores: lds byte j + head holds
+// src[start + j]; returns head (< 16).  LDS needs head + len + 15 bytes.
+__device__ __forceinline__ int stage_bytes(const uint8_t* __restrict__ src,
+                                          int64_t nbytes, int64_t start,
+                                          int len, uint4* lds) {
+  const int64_t base = start & ~(int64_t)15;
+  const int head = (int)(start - base);
+  const int nq = (head + len + 15) >> 4;
+  int64_t full = (nbytes - base) >> 4;            // quads wholly inside src
+  const int nfull = full < nq ? (int)full : nq;
+  const uint4* q = reinterpret_cast<const uint4*>(src + base);
+  constexpr int kU = 4;      // loads in flight per thread before the stores
+  const int bd = blockDim.x;
+  int i = threadIdx.x;
+  for (; i + (kU - 1) * bd < nfull; i += kU * bd) {
+    uint4 v[kU];
+#pragma unroll
+    for (int j = 0; j < kU; ++j) v[j] = q[i + j * bd];
+#pragma unroll
+    for (int j = 0; j < kU; ++j) lds[i + j * bd] = v[j];
+  }
+  for (; i < nfull; i += bd) lds[i] = q[i];
+  // at most one quad runs past the end of src: byte loads
+  for (int i = nfull + (int)threadIdx.x; i < nq; i += blockDim.x) {
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 16; ++k) {
+      const int64_t a = base + 16 * (int64_t)i + k;
+      if (a < nbytes) w[k >> 2] |= (uint32_t)src[a] << (8 * (k & 3));
+    }
+    lds[i] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  return head;
+}
+
+// Row pass: block (8 input rows, image b).  The rows (contiguous in the
+// packed HWC image) and the image's horizontal coefficient table are staged
+// in LDS; a thread produces all 3 channels of one output column of a row,
+// so each fixed-point coefficient is read once for 3 multiply-adds.
+template <bool kCoefInLds>
 __global__ __launch_bounds__(256) void resize_rows_kernel(
-    const uint8_t* __restrict__ images, const int64_t* __restrict__ meta,
-    const int32_t* __restrict__ coef, uint8_t* __restrict__ tmp, int S, int KS) {
-  const int y = blockIdx.x, b = blockIdx.y;
+    const uint8_t* __restrict__ images, int64_t nbytes,
+    const int64_t* __restrict__ meta, const int32_t* __restrict__ coef,
+    uint8_t* __restrict__ tmp, int S, int KS) {
+  __shared__ uint4 spix[kResizeLds / 16];
+  __shared__ uint4 scoef[kCoefInLds ? kResizeCoefLds / 16 : 1];
+  const int b = blockIdx.y;
   const int H = (int)meta[b * 4 + 1], W = (int)meta[b * 4 + 2];
-  if (y >= H) return;
-  const uint8_t* src = images + meta[b * 4 + 0] + (int64_t)y * W * 3;
-  uint8_t* dst = tmp + meta[b * 4 + 3] + (int64_t)y * S * 3;
-  const int32_t* tab = coef + (int64_t)(b * 2 + 0) * S * (2 + KS);
-  for (int o = threadIdx.x; o < S * 3; o += 256) {
-    const int xx = o / 3, c = o - xx * 3;
-    const int32_t* row = tab + (int64_t)xx * (2 + KS);
-    const int xmin = row[0], n = row[1];
-    int32_t acc = 1 << 21;
-    for (int x = 0; x < n; ++x) acc += (int32_t)src[(xmin + x) * 3 + c] * row[2 + x];
-    dst[o] = pil_clip8(acc);
+  const int y0 = blockIdx.x * kResizeRows;
+  if (y0 >= H) return;
+  const int rb = W * 3, ld = 2 + KS;
+  const int64_t tab_off = (int64_t)(b * 2 + 0) * S * ld;
+  const int32_t* ct = coef + tab_off;
+  if (kCoefInLds) {    // host: S * ld * 4 <= kResizeCoefLds - 32
+    const int64_t coef_bytes = (int64_t)gridDim.y * 2 * S * ld * 4;
+    const int h = stage_bytes(reinterpret_cast<const uint8_t*>(coef), coef_bytes,
+                              tab_off * 4, S * ld * 4, scoef);
+    ct = reinterpret_cast<const int32_t*>(reinterpret_cast<const uint8_t*>(scoef) + h);
+  }
+  const int nrows = min(kResizeRows, H - y0);
+  const int fit = (kResizeLds - 32) / rb;           // host: rb <= kResizeLds - 32
+  uint8_t* dst = tmp + meta[b * 4 + 3];
+  for (int r0 = 0; r0 < nrows; r0 += fit) {
+    const int nr = min(fit, nrows - r0);
+    const int head = stage_bytes(images, nbytes,
+                                 meta[b * 4 + 0] + (int64_t)(y0 + r0) * rb,
+                                 nr * rb, spix);
+    __syncthreads();
+    const uint8_t* pix = reinterpret_cast<const uint8_t*>(spix) + head;
+    for (int o = threadIdx.x; o < nr * S; o += 256) {
+      const int r = o / S, xx = o - r * S;
+      const int32_t* row = ct + xx * ld;
+      const int xmin = row[0], n = row[1];
+      const uint8_t* px = pix + r * rb + xmin * 3;
+      int32_t a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+      // taps in fours: rows are zero-padded to KS % 4 == 0, and the staged
+      // LDS region has slack, so the extra taps add 0 * (in-bounds bytes)
+      for (int x = 0; x < n; x += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t k = row[2 + x + u];
+          a0 += __mul24((int32_t)px[3 * (x + u) + 0], k);   // |k| < 2^23
+          a1 += __mul24((int32_t)px[3 * (x + u) + 1], k);
+          a2 += __mul24((int32_t)px[3 * (x + u) + 2], k);
+        }
+      }
+      uint8_t* d = dst + ((int64_t)(y0 + r0 + r) * S + xx) * 3;
+      d[0] = pil_clip8(a0);
+      d[1] = pil_clip8(a1);
+      d[2] = pil_clip8(a2);
+    }
+    __syncthreads();
   }
 }
 
-// Column pass + ToTensor: block (output row yy, image b); threads over
-// (c, xx) so each channel plane row is written contiguously.
+// Column pass + ToTensor: block (8 output rows, image b).  The union of the
+// row-pass rows those outputs read is staged in LDS when it fits (else read
+// from global), with the 8 coefficient rows; a thread produces the 3
+// channels of one output pixel (each coefficient read once for 3
+// multiply-adds) and writes them to the 3 fp32 planes, coalesced over xx.
 __global__ __launch_bounds__(256) void resize_cols_kernel(
-    const uint8_t* __restrict__ tmp, const int64_t* __restrict__ meta,
-    const int32_t* __restrict__ coef, float* __restrict__ out, int S, int KS) {
-  const int yy = blockIdx.x, b = blockIdx.y;
-  const uint8_t* src = tmp + meta[b * 4 + 3];
-  const int32_t* row = coef + ((int64_t)(b * 2 + 1) * S + yy) * (2 + KS);
-  const int ymin = row[0], n = row[1];
-  for (int o = threadIdx.x; o < S * 3; o += 256) {
-    const int c = o / S, xx = o - c * S;
-    int32_t acc = 1 << 21;
-    for (int y = 0; y < n; ++y)
-      acc += (int32_t)src[((int64_t)(ymin + y) * S + xx) * 3 + c] * row[2 + y];
-    out[(((int64_t)b * 3 + c) * S + yy) * S + xx] = (float)pil_clip8(acc) / 255.0f;
+    const uint8_t* __restrict__ tmp, int64_t tmp_bytes,
+    const int64_t* __restrict__ meta, const int32_t* __restrict__ coef,
+    float* __restrict__ out, int S, int KS) {
+  __shared__ uint4 spix[kResizeLds / 16];
+  __shared__ int32_t scoef[kResizeOutRows * (2 + kResizeMaxKS)];
+  const int b = blockIdx.y;
+  const int yy0 = blockIdx.x * kResizeOutRows;
+  const int ld = 2 + KS, rb = S * 3;
+  const int nout = min(kResizeOutRows, S - yy0);
+  const int32_t* tab = coef + ((int64_t)(b * 2 + 1) * S + yy0) * ld;
+  const bool coef_lds = KS <= kResizeMaxKS;
+  for (int i = threadIdx.x; coef_lds && i < nout * ld; i += 256) scoef[i] = tab[i];
+  const int32_t* ct = coef_lds ? scoef : tab;
+  const int lo = tab[0];
+  const int hi = tab[(nout - 1) * ld] + tab[(nout - 1) * ld + 1];
+  const bool staged = (int64_t)(hi - lo + 3) * rb <= kResizeLds - 32;
+  int head = 0;
+  if (staged)
+    head = stage_bytes(tmp, tmp_bytes, meta[b * 4 + 3] + (int64_t)lo * rb,
+                       (hi - lo) * rb, spix);
+  __syncthreads();
+  const uint8_t* base = staged ? reinterpret_cast<const uint8_t*>(spix) + head
+                               : tmp + meta[b * 4 + 3] + (int64_t)lo * rb;
+  float* plane = out + (int64_t)b * 3 * S * S;
+  for (int o = threadIdx.x; o < nout * S; o += 256) {
+    const int r = o / S, xx = o - r * S;
+    const int32_t* row = ct + r * ld;
+    const int ymin = row[0] - lo, n = row[1];
+    const uint8_t* px = base + (int64_t)ymin * rb + xx * 3;
+    int32_t a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+    if (staged) {      // taps in fours over zero-padded rows (3 rows of slack)
+      for (int y = 0; y < n; y += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t k = row[2 + y + u];
+          const uint8_t* p = px + (y + u) * rb;
+          a0 += __mul24((int32_t)p[0], k);
+          a1 += __mul24((int32_t)p[1], k);
+          a2 += __mul24((int32_t)p[2], k);
+        }
+      }
+    } else {
+      for (int y = 0; y < n; ++y) {
+        const int32_t k = row[2 + y];
+        const uint8_t* p = px + (int64_t)y * rb;
+        a0 += __mul24((int32_t)p[0], k);
+        a1 += __mul24((int32_t)p[1], k);
+        a2 += __mul24((int32_t)p[2], k);
+      }
+    }
+    const int64_t at = (int64_t)(yy0 + r) * S + xx;
+    plane[at] = (float)pil_clip8(a0) / 255.0f;
+    plane[(int64_t)S * S + at] = (float)pil_clip8(a1) / 255.0f;
+    plane[(int64_t)2 * S * S + at] = (float)pil_clip8(a2) / 255.0f;
   }
 }
 
@@ -220,21 +347,31 @@ int cadence_vit_features(const float* resid, void* out, int64_t ldo,
   return (int)hipGetLastError();
 }
 
-int cadence_resize_bicubic(const void* images, const int64_t* meta, int64_t B,
-                           int64_t S, int64_t KS, int64_t max_h, void* coef,
-                           void* tmp, float* out, void* stream) {
+int cadence_resize_bicubic(const void* images, int64_t images_bytes,
+                           const int64_t* meta, int64_t B, int64_t S,
+                           int64_t KS, int64_t max_h, int64_t max_w, void* coef,
+                           void* tmp, int64_t tmp_bytes, float* out,
+                           void* stream) {
   if (B <= 0) return 0;
-  if (S <= 0 || KS < 5 || max_h <= 0) return (int)hipErrorInvalidValue;
+  if (S <= 0 || KS < 5 || KS % 4 || max_h <= 0 || max_w <= 0 ||
+      max_w * 3 > kResizeLds - 32 || S * 3 > kResizeLds - 32)
+    return (int)hipErrorInvalidValue;
   hipStream_t s = static_cast<hipStream_t>(stream);
   int32_t* tab = static_cast<int32_t*>(coef);
+  const uint8_t* img = static_cast<const uint8_t*>(images);
+  uint8_t* t = static_cast<uint8_t*>(tmp);
   hipLaunchKernelGGL(resize_coeff_kernel, dim3((S + 255) / 256, 2, B), dim3(256),
                      0, s, meta, tab, (int)S, (int)KS);
-  hipLaunchKernelGGL(resize_rows_kernel, dim3(max_h, B), dim3(256), 0, s,
-                     static_cast<const uint8_t*>(images), meta, tab,
-                     static_cast<uint8_t*>(tmp), (int)S, (int)KS);
-  hipLaunchKernelGGL(resize_cols_kernel, dim3(S, B), dim3(256), 0, s,
-                     static_cast<const uint8_t*>(tmp), meta, tab, out, (int)S,
-                     (int)KS);
+  const dim3 rgrid((max_h + kResizeRows - 1) / kResizeRows, B);
+  if (S * (2 + KS) * 4 <= kResizeCoefLds - 32)
+    hipLaunchKernelGGL(resize_rows_kernel<true>, rgrid, dim3(256), 0, s, img,
+                       images_bytes, meta, tab, t, (int)S, (int)KS);
+  else
+    hipLaunchKernelGGL(resize_rows_kernel<false>, rgrid, dim3(256), 0, s, img,
+                       images_bytes, meta, tab, t, (int)S, (int)KS);
+  hipLaunchKernelGGL(resize_cols_kernel,
+                     dim3((S + kResizeOutRows - 1) / kResizeOutRows, B), dim3(256),
+                     0, s, t, tmp_bytes, meta, tab, out, (int)S, (int)KS);
   return (int)hipGetLastError();
 }
 

@@ -340,16 +340,20 @@ int cadence_vit_features(const float* resid, void* out, int64_t ldo,
  * BICUBIC) on a PIL RGB image + ToTensor (dino_siglip.py:12-16, 88-124,
  * 148-151; both encoders' transforms share it), i.e. Pillow's
  * ImagingResample (libImaging/Resample.c) bit for bit, for a ragged batch:
- *   images  packed uint8 HWC RGB; meta[b] = {byte offset, H, W, tmp offset}
- *   KS      taps per coefficient row >= 2 * ceil(2 * max(in / S, 1)) + 1 over
- *           every image side (host computes it)
+ *   images  packed uint8 HWC RGB, images_bytes long; meta[b] = {byte offset,
+ *           H, W, tmp offset}; every W <= max_w <= 10912, S <= 10912;
+ *           images, coef and tmp 16-byte aligned
+ *   KS      taps per coefficient row, a multiple of 4 >= 2 * ceil(2 *
+ *           max(in / S, 1)) + 1 over every image side (host computes it)
  *   coef    workspace, B * 2 * S * (2 + KS) int32
- *   tmp     workspace, sum_b H_b * S * 3 bytes (the row-pass images)
+ *   tmp     workspace, tmp_bytes >= sum_b H_b * S * 3 (row-pass images)
  *   out     [B, 3, S, S] fp32 in [0, 1]
  * Replaces the host PIL resize per image in VisionEncoder.forward. */
-int cadence_resize_bicubic(const void* images, const int64_t* meta, int64_t B,
-                           int64_t S, int64_t KS, int64_t max_h, void* coef,
-                           void* tmp, float* out, void* stream);
+int cadence_resize_bicubic(const void* images, int64_t images_bytes,
+                           const int64_t* meta, int64_t B, int64_t S,
+                           int64_t KS, int64_t max_h, int64_t max_w, void* coef,
+                           void* tmp, int64_t tmp_bytes, float* out,
+                           void* stream);
 
 /* ---- misc ------------------------------------------------------------------ */
 

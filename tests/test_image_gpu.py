@@ -42,6 +42,13 @@ def test_resize_ragged_batch_bitexact(dev, size):
   for i, a in enumerate(imgs):
     want = R.pil_resize_to_tensor(a, size)
     assert torch.equal(got[i], want), (shapes[i], size)
+  # small images only: the coefficient tables fit in LDS (the batch above
+  # takes the global-table path) and every column pass is LDS-staged
+  small = [(480, 640), (300, 200), (size, size), (3, 5)]
+  imgs = _images(rng, small)
+  got = image_io.resize_arrays(imgs, size, dev).cpu()
+  for i, a in enumerate(imgs):
+    assert torch.equal(got[i], R.pil_resize_to_tensor(a, size)), (small[i], size)
 
 
 def test_resize_rejects_bad_input(dev):
@@ -49,6 +56,8 @@ def test_resize_rejects_bad_input(dev):
     image_io.resize_arrays([np.zeros((4, 4), np.uint8)], 224, dev)
   with pytest.raises(ValueError):
     image_io.resize_arrays([], 224, dev)
+  with pytest.raises(RuntimeError):     # wider than one LDS-staged row
+    image_io.resize_arrays([np.zeros((2, 11000, 3), np.uint8)], 224, dev)
 
 
 def test_img_path_list_feeds_the_model(dev, tmp_path):
