@@ -470,16 +470,19 @@ def image_tokens(pixels, p, vcfg):
 # ---------------------------------------------------------------- sampler
 
 def greedy_sample(p, cfg, prompt_tokens, steps, pixels=None, vcfg=None,
-                  compat=True):
+                  compat=True, lengths=None):
   """examples/cadence_sampler.py:185-298 + :112-182 (greedy, no EOS stop).
 
-  Prompts are equal length (no padding), positions arange(T).  Prefill runs
+  Prompts are equal length (positions arange(T)) unless `lengths` gives
+  left-padded lengths (pads at position -1).  Prefill runs
   tokens[:, :-1] (+ image), then one cached step on the last prompt token,
   then `steps - 1` decode steps.  Returns the generated tokens [B, steps]
   and the per-step logits [B, steps, V].
   """
   b, t = prompt_tokens.shape
   pos = torch.arange(t, dtype=torch.int32)[None].expand(b, -1).contiguous()
+  if lengths is not None:   # left-padded prompts (cadence_sampler.py:198-201)
+    pos = torch.clip(pos - t + lengths.to(torch.int32)[:, None], min=-1)
   img = image_tokens(pixels, p, vcfg) if pixels is not None else None
   if t > 1:
     _, cache = griffin_forward(p, cfg, prompt_tokens[:, :-1], pos[:, :-1],
