@@ -20,6 +20,7 @@ from . import modules
 from . import griffin
 from . import sampler
 from . import vision
+from . import checkpoint
 
 ScanType = common.ScanType
 TemporalBlockType = common.TemporalBlockType
@@ -46,6 +47,8 @@ Sampler = sampler.Sampler
 SamplerOutput = sampler.SamplerOutput
 VisionEncoder = vision.VisionEncoder
 MLPProjector = vision.MLPProjector
+load_params = checkpoint.load_params
+load_griffin = checkpoint.load_griffin
 
 __all__ = (
     "ScanType",
