@@ -60,6 +60,66 @@ def gather_rows(local: torch.Tensor) -> torch.Tensor:
   return out
 
 
+# ------------------------------------------- sequence-parallel RG-LRU scan
+#
+# SURVEY §8f f4: one long sequence split over the ranks in order (rank r
+# holds timesteps [r*Lr, (r+1)*Lr)).  The recurrence h_t = a_t h_{t-1} + x_t
+# (reference layers.py:145-199; `a <- a * ~reset`) is affine in its initial
+# state, so a chunk is summarised by two [B, E] fp32 vectors: h_loc (its end
+# state from h = 0) and P (the product of its a_t, zeroed by a reset; the
+# end state of the same scan with x = 0 from h = 1).  One all-gather of the
+# (h_loc, P) pairs gives every rank its carry-in
+#     h_in[0] = h0,  h_in[r+1] = P[r] * h_in[r] + h_loc[r]   (fp32),
+# and a second local scan from h_in[r] writes the outputs.  The same algebra
+# as the reference's Pallas/JAX chunked scan (recurrentgemma/jax/scan.py:
+# 207-347, jax/pallas.py:71-193); within a chunk the op order is the
+# reference's, only the carry composition differs (fp32 rounding).
+# The local scans are the HIP `rnn_scan` kernel; the combine is R fused
+# multiply-adds on [B, E] (host-orchestrated torch ops on the device).
+
+def sp_scan_stats(x, a, reset, scan=None) -> torch.Tensor:
+  """[2, B, E] fp32: (h_loc, P) of this rank's chunk."""
+  if scan is None:
+    from .layers import rnn_scan as scan
+  b, _, e = x.shape
+  _, h_loc = scan(x, a, reset, None)
+  _, prod = scan(torch.zeros_like(x), a, reset,
+                 torch.ones(b, e, dtype=torch.float32, device=x.device))
+  return torch.stack([h_loc, prod])
+
+
+def sp_carry_in(stats_all: torch.Tensor, rank: int, h0=None) -> torch.Tensor:
+  """Carry-in of chunk `rank` from every chunk's (h_loc, P) [R, 2, B, E]."""
+  h = (torch.zeros_like(stats_all[0, 0]) if h0 is None
+       else h0.to(torch.float32).clone())
+  for r in range(rank):
+    h = stats_all[r, 1] * h + stats_all[r, 0]
+  return h
+
+
+def sequence_parallel_rnn_scan(x, a, reset, h0=None, group=None, scan=None):
+  """`rnn_scan` over a sequence sharded by timestep across the ranks of
+  `group` (rank order = sequence order).  x, a: [B, Lr, E] (this rank's
+  chunk), reset: [B, Lr], h0: [B, E] fp32 initial state of the whole
+  sequence (used by rank 0) or None.  Returns (y [B, Lr, E], h_last [B, E]
+  of this chunk; the last rank's is the sequence's)."""
+  if scan is None:
+    from .layers import rnn_scan as scan
+  stats = sp_scan_stats(x, a, reset, scan)
+  if dist.is_available() and dist.is_initialized():
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    out = torch.empty((world,) + tuple(stats.shape), dtype=stats.dtype,
+                      device=stats.device)
+    if dist.get_backend(group) == "gloo":
+      dist.all_gather(list(out.unbind(0)), stats, group=group)
+    else:
+      dist.all_gather_into_tensor(out, stats, group=group)
+  else:
+    rank, out = 0, stats[None]
+  h_in = sp_carry_in(out, rank, h0)
+  return scan(x, a, reset, h_in)
+
+
 def barrier() -> None:
   if dist.is_available() and dist.is_initialized():
     dist.barrier()

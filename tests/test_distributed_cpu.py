@@ -61,3 +61,69 @@ def test_shard_range_contract():
   assert D.shard_range(256, 3, 8) == (96, 128)
   with pytest.raises(ValueError):
     D.shard_range(10, 0, 4)
+
+
+# ------------------------------------------- sequence-parallel RG-LRU scan
+
+def _sp_inputs(b=2, t=96, e=16, seed=5):
+  g = torch.Generator().manual_seed(seed)
+  x = torch.randn(b, t, e, generator=g).to(torch.bfloat16)
+  a = (0.5 + 0.5 * torch.rand(b, t, e, generator=g)).to(torch.bfloat16)
+  reset = torch.rand(b, t, generator=g) < 0.03
+  h0 = torch.randn(b, e, generator=g)
+  return x, a, reset, h0
+
+
+def _sp_worker(rank, world, port, q):
+  from oracle import griffin_ref as R
+  os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+  D.init_from_env(backend="gloo")
+  x, a, reset, h0 = _sp_inputs()
+  lr = x.shape[1] // world
+  sl = slice(rank * lr, (rank + 1) * lr)
+  y, h = D.sequence_parallel_rnn_scan(x[:, sl], a[:, sl], reset[:, sl],
+                                      h0 if rank == 0 else None, scan=R.rnn_scan)
+  q.put((rank, y, h))
+  D.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sequence_parallel_scan_gloo(world):
+  """SURVEY 8f f4 over gloo, the oracle scan standing in for the kernel:
+  equals the single-sequence scan up to fp32 rounding of the carry."""
+  from oracle import griffin_ref as R
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_sp_worker, args=(r, world, port, q))
+           for r in range(world)]
+  for p in procs:
+    p.start()
+  res = sorted([q.get(timeout=120) for _ in procs], key=lambda r: r[0])
+  for p in procs:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  x, a, reset, h0 = _sp_inputs()
+  y_ref, h_ref = R.rnn_scan(x, a, reset, h0)
+  y = torch.cat([r[1] for r in res], dim=1)
+  assert (y == y_ref).float().mean().item() > 0.99
+  torch.testing.assert_close(y.float(), y_ref.float(), rtol=1e-2, atol=1e-2)
+  torch.testing.assert_close(res[-1][2], h_ref, rtol=1e-5, atol=1e-5)
+
+
+def test_sp_carry_algebra_single_process():
+  """sp_scan_stats + sp_carry_in per chunk == one scan (oracle scan)."""
+  from oracle import griffin_ref as R
+  x, a, reset, h0 = _sp_inputs(t=120)
+  chunks = 5
+  lr = x.shape[1] // chunks
+  sls = [slice(i * lr, (i + 1) * lr) for i in range(chunks)]
+  stats = torch.stack([D.sp_scan_stats(x[:, s], a[:, s], reset[:, s], R.rnn_scan)
+                       for s in sls])
+  ys = [R.rnn_scan(x[:, s], a[:, s], reset[:, s], D.sp_carry_in(stats, i, h0))
+        for i, s in enumerate(sls)]
+  y_ref, h_ref = R.rnn_scan(x, a, reset, h0)
+  torch.testing.assert_close(torch.cat([y for y, _ in ys], 1).float(),
+                             y_ref.float(), rtol=1e-2, atol=1e-2)
+  torch.testing.assert_close(ys[-1][1], h_ref, rtol=1e-5, atol=1e-5)

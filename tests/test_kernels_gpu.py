@@ -436,3 +436,31 @@ def test_library_uses_torch_hip_runtime(dev):
   _lib.load()
   rts = _lib.hip_runtimes_loaded()
   assert len(rts) == 1, rts
+
+
+def test_sequence_parallel_scan_chunks_on_gpu(dev):
+  """SURVEY 8f f4 carry algebra with the HIP scan, 4 chunks simulated on one
+  GPU (the collective is the gloo-tested all-gather): equals the one-pass
+  HIP scan up to fp32 rounding of the carry composition."""
+  from cadence import distributed as D
+  g = torch.Generator().manual_seed(17)
+  b, t, e, chunks = 2, 4096, 2560, 4
+  x = rnd(b, t, e, gen=g).to(dev)
+  a = (0.9 + 0.1 * torch.rand(b, t, e, generator=g)).to(BF).to(dev)
+  reset = (torch.rand(b, t, generator=g) < 0.001).to(dev)
+  h0 = torch.randn(b, e, generator=g).to(dev)
+  lr = t // chunks
+  sls = [slice(i * lr, (i + 1) * lr) for i in range(chunks)]
+  stats = torch.stack([D.sp_scan_stats(x[:, s].contiguous(), a[:, s].contiguous(),
+                                       reset[:, s].contiguous()) for s in sls])
+  ys, hs = [], []
+  for i, s in enumerate(sls):
+    y, h = cadence.rnn_scan(x[:, s].contiguous(), a[:, s].contiguous(),
+                            reset[:, s].contiguous(), D.sp_carry_in(stats, i, h0))
+    ys.append(y)
+    hs.append(h)
+  y_ref, h_ref = cadence.rnn_scan(x, a, reset, h0)
+  y = torch.cat(ys, 1)
+  assert (y == y_ref).float().mean().item() > 0.99
+  torch.testing.assert_close(y.float(), y_ref.float(), rtol=1e-2, atol=1e-2)
+  torch.testing.assert_close(hs[-1], h_ref, rtol=1e-4, atol=1e-4)
