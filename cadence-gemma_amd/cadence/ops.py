@@ -792,9 +792,6 @@ def _im2col(pixels, mean, std, patch, kpad):
   return out
 
 
-RESIZE_MAX_ROW_BYTES = 32768 - 32   # one pixel row staged in LDS (vision.hip)
-
-
 def resize_taps(in_size: int, size: int) -> int:
   """Pillow precompute_coeffs ksize for one image side (Resample.c):
   ceil(2 * max(in / S, 1)) * 2 + 1, in the same double arithmetic."""
@@ -810,8 +807,6 @@ def _resize_bicubic(images, meta, S, KS, max_h, max_w, tmp_bytes):
   _need(meta.dtype == torch.int64 and meta.dim() == 2 and meta.shape[1] == 4
         and meta.is_contiguous() and meta.device == images.device,
         "meta [B, 4] int64 on the images' device")
-  _need(3 * max_w <= RESIZE_MAX_ROW_BYTES and 3 * S <= RESIZE_MAX_ROW_BYTES,
-        f"image width and S must be <= {RESIZE_MAX_ROW_BYTES // 3}")
   B = meta.shape[0]
   KS = (KS + 3) // 4 * 4            # coefficient rows padded to whole fours
   out = torch.empty(B, 3, S, S, dtype=_F32, device=images.device)

@@ -135,10 +135,8 @@ __device__ __forceinline__ uint8_t pil_clip8(int32_t ss) {
 }
 
 constexpr int kResizeRows = 8;          // input rows per row-pass block
-constexpr int kResizeOutRows = 8;       // output rows per column-pass block
-constexpr int kResizeLds = 32768;       // staged pixel bytes per block
-constexpr int kResizeCoefLds = 32768;   // coefficient table bytes (if it fits)
-constexpr int kResizeMaxKS = 126;       // column-pass coefficient rows in LDS
+constexpr int kResizeLds = 16384;       // staged pixel bytes per block
+constexpr int kResizeCoefLds = 16384;   // coefficient table bytes (if it fits)
 
 // Loads bytes [start, start + len) of `src` (valid up to `nbytes`; `src`
 // 16-byte aligned) into LDS as aligned 16-byte quads, all of a thread's
@@ -201,23 +199,18 @@ __global__ __launch_bounds__(256) void resize_rows_kernel(
     ct = reinterpret_cast<const int32_t*>(reinterpret_cast<const uint8_t*>(scoef) + h);
   }
   const int nrows = min(kResizeRows, H - y0);
-  const int fit = (kResizeLds - 32) / rb;           // host: rb <= kResizeLds - 32
   uint8_t* dst = tmp + meta[b * 4 + 3];
-  for (int r0 = 0; r0 < nrows; r0 += fit) {
-    const int nr = min(fit, nrows - r0);
-    const int head = stage_bytes(images, nbytes,
-                                 meta[b * 4 + 0] + (int64_t)(y0 + r0) * rb,
-                                 nr * rb, spix);
-    __syncthreads();
-    const uint8_t* pix = reinterpret_cast<const uint8_t*>(spix) + head;
-    for (int o = threadIdx.x; o < nr * S; o += 256) {
-      const int r = o / S, xx = o - r * S;
-      const int32_t* row = ct + xx * ld;
-      const int xmin = row[0], n = row[1];
-      const uint8_t* px = pix + r * rb + xmin * 3;
-      int32_t a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
-      // taps in fours: rows are zero-padded to KS % 4 == 0, and the staged
-      // LDS region has slack, so the extra taps add 0 * (in-bounds bytes)
+  // rows wider than the LDS buffer (W > 5450) are read from global directly
+  const bool staged = rb <= kResizeLds - 32;
+  const int fit = staged ? (kResizeLds - 32) / rb : nrows;
+  // one output pixel (3 channels) of row-pass row r; PX is the LDS image
+  // (taps in fours: tables are zero-padded to KS % 4 == 0 and the staged
+  // region has slack, so extra taps add 0 * in-bounds bytes) or, for rows
+  // too wide to stage, the global image (exact tap count)
+  auto pixel = [&](const uint8_t* px, const int32_t* row, int n, bool four,
+                   uint8_t* d) {
+    int32_t a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
+    if (four) {
       for (int x = 0; x < n; x += 4) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -227,75 +220,70 @@ __global__ __launch_bounds__(256) void resize_rows_kernel(
           a2 += __mul24((int32_t)px[3 * (x + u) + 2], k);
         }
       }
-      uint8_t* d = dst + ((int64_t)(y0 + r0 + r) * S + xx) * 3;
-      d[0] = pil_clip8(a0);
-      d[1] = pil_clip8(a1);
-      d[2] = pil_clip8(a2);
+    } else {
+      for (int x = 0; x < n; ++x) {
+        const int32_t k = row[2 + x];
+        a0 += __mul24((int32_t)px[3 * x + 0], k);
+        a1 += __mul24((int32_t)px[3 * x + 1], k);
+        a2 += __mul24((int32_t)px[3 * x + 2], k);
+      }
     }
-    __syncthreads();
+    d[0] = pil_clip8(a0);
+    d[1] = pil_clip8(a1);
+    d[2] = pil_clip8(a2);
+  };
+  for (int r0 = 0; r0 < nrows; r0 += fit) {
+    const int nr = min(fit, nrows - r0);
+    const int64_t src0 = meta[b * 4 + 0] + (int64_t)(y0 + r0) * rb;
+    if (staged) {
+      const int head = stage_bytes(images, nbytes, src0, nr * rb, spix);
+      __syncthreads();
+      const uint8_t* pix = reinterpret_cast<const uint8_t*>(spix) + head;
+      for (int o = threadIdx.x; o < nr * S; o += 256) {
+        const int r = o / S, xx = o - r * S;
+        const int32_t* row = ct + xx * ld;
+        pixel(pix + r * rb + row[0] * 3, row, row[1], true,
+              dst + ((int64_t)(y0 + r0 + r) * S + xx) * 3);
+      }
+      __syncthreads();
+    } else {
+      for (int o = threadIdx.x; o < nr * S; o += 256) {
+        const int r = o / S, xx = o - r * S;
+        const int32_t* row = ct + xx * ld;
+        pixel(images + src0 + (int64_t)r * rb + row[0] * 3, row, row[1], false,
+              dst + ((int64_t)(y0 + r0 + r) * S + xx) * 3);
+      }
+    }
   }
 }
 
-// Column pass + ToTensor: block (8 output rows, image b).  The union of the
-// row-pass rows those outputs read is staged in LDS when it fits (else read
-// from global), with the 8 coefficient rows; a thread produces the 3
-// channels of one output pixel (each coefficient read once for 3
-// multiply-adds) and writes them to the 3 fp32 planes, coalesced over xx.
+// Column pass + ToTensor: block (output row yy, image b); the coefficient
+// row is block-uniform (scalar loads); a thread produces the 3 channels of
+// one output pixel from the L2-resident row-pass image (each coefficient
+// read once for 3 multiply-adds) and writes the 3 fp32 planes, coalesced
+// over xx.
 __global__ __launch_bounds__(256) void resize_cols_kernel(
-    const uint8_t* __restrict__ tmp, int64_t tmp_bytes,
-    const int64_t* __restrict__ meta, const int32_t* __restrict__ coef,
-    float* __restrict__ out, int S, int KS) {
-  __shared__ uint4 spix[kResizeLds / 16];
-  __shared__ int32_t scoef[kResizeOutRows * (2 + kResizeMaxKS)];
-  const int b = blockIdx.y;
-  const int yy0 = blockIdx.x * kResizeOutRows;
+    const uint8_t* __restrict__ tmp, const int64_t* __restrict__ meta,
+    const int32_t* __restrict__ coef, float* __restrict__ out, int S, int KS) {
+  const int yy = blockIdx.x, b = blockIdx.y;
   const int ld = 2 + KS, rb = S * 3;
-  const int nout = min(kResizeOutRows, S - yy0);
-  const int32_t* tab = coef + ((int64_t)(b * 2 + 1) * S + yy0) * ld;
-  const bool coef_lds = KS <= kResizeMaxKS;
-  for (int i = threadIdx.x; coef_lds && i < nout * ld; i += 256) scoef[i] = tab[i];
-  const int32_t* ct = coef_lds ? scoef : tab;
-  const int lo = tab[0];
-  const int hi = tab[(nout - 1) * ld] + tab[(nout - 1) * ld + 1];
-  const bool staged = (int64_t)(hi - lo + 3) * rb <= kResizeLds - 32;
-  int head = 0;
-  if (staged)
-    head = stage_bytes(tmp, tmp_bytes, meta[b * 4 + 3] + (int64_t)lo * rb,
-                       (hi - lo) * rb, spix);
-  __syncthreads();
-  const uint8_t* base = staged ? reinterpret_cast<const uint8_t*>(spix) + head
-                               : tmp + meta[b * 4 + 3] + (int64_t)lo * rb;
-  float* plane = out + (int64_t)b * 3 * S * S;
-  for (int o = threadIdx.x; o < nout * S; o += 256) {
-    const int r = o / S, xx = o - r * S;
-    const int32_t* row = ct + r * ld;
-    const int ymin = row[0] - lo, n = row[1];
-    const uint8_t* px = base + (int64_t)ymin * rb + xx * 3;
+  const int32_t* row = coef + ((int64_t)(b * 2 + 1) * S + yy) * ld;
+  const int ymin = row[0], n = row[1];
+  const uint8_t* src = tmp + meta[b * 4 + 3] + (int64_t)ymin * rb;
+  float* plane = out + (int64_t)b * 3 * S * S + (int64_t)yy * S;
+  for (int xx = threadIdx.x; xx < S; xx += 256) {
+    const uint8_t* px = src + xx * 3;
     int32_t a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21;
-    if (staged) {      // taps in fours over zero-padded rows (3 rows of slack)
-      for (int y = 0; y < n; y += 4) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int32_t k = row[2 + y + u];
-          const uint8_t* p = px + (y + u) * rb;
-          a0 += __mul24((int32_t)p[0], k);
-          a1 += __mul24((int32_t)p[1], k);
-          a2 += __mul24((int32_t)p[2], k);
-        }
-      }
-    } else {
-      for (int y = 0; y < n; ++y) {
-        const int32_t k = row[2 + y];
-        const uint8_t* p = px + (int64_t)y * rb;
-        a0 += __mul24((int32_t)p[0], k);
-        a1 += __mul24((int32_t)p[1], k);
-        a2 += __mul24((int32_t)p[2], k);
-      }
+    for (int y = 0; y < n; ++y) {
+      const int32_t k = row[2 + y];
+      const uint8_t* p = px + (int64_t)y * rb;
+      a0 += __mul24((int32_t)p[0], k);
+      a1 += __mul24((int32_t)p[1], k);
+      a2 += __mul24((int32_t)p[2], k);
     }
-    const int64_t at = (int64_t)(yy0 + r) * S + xx;
-    plane[at] = (float)pil_clip8(a0) / 255.0f;
-    plane[(int64_t)S * S + at] = (float)pil_clip8(a1) / 255.0f;
-    plane[(int64_t)2 * S * S + at] = (float)pil_clip8(a2) / 255.0f;
+    plane[xx] = (float)pil_clip8(a0) / 255.0f;
+    plane[(int64_t)S * S + xx] = (float)pil_clip8(a1) / 255.0f;
+    plane[(int64_t)2 * S * S + xx] = (float)pil_clip8(a2) / 255.0f;
   }
 }
 
@@ -353,8 +341,7 @@ int cadence_resize_bicubic(const void* images, int64_t images_bytes,
                            void* tmp, int64_t tmp_bytes, float* out,
                            void* stream) {
   if (B <= 0) return 0;
-  if (S <= 0 || KS < 5 || KS % 4 || max_h <= 0 || max_w <= 0 ||
-      max_w * 3 > kResizeLds - 32 || S * 3 > kResizeLds - 32)
+  if (S <= 0 || KS < 5 || KS % 4 || max_h <= 0 || max_w <= 0 || tmp_bytes <= 0)
     return (int)hipErrorInvalidValue;
   hipStream_t s = static_cast<hipStream_t>(stream);
   int32_t* tab = static_cast<int32_t*>(coef);
@@ -369,9 +356,8 @@ int cadence_resize_bicubic(const void* images, int64_t images_bytes,
   else
     hipLaunchKernelGGL(resize_rows_kernel<false>, rgrid, dim3(256), 0, s, img,
                        images_bytes, meta, tab, t, (int)S, (int)KS);
-  hipLaunchKernelGGL(resize_cols_kernel,
-                     dim3((S + kResizeOutRows - 1) / kResizeOutRows, B), dim3(256),
-                     0, s, t, tmp_bytes, meta, tab, out, (int)S, (int)KS);
+  hipLaunchKernelGGL(resize_cols_kernel, dim3(S, B), dim3(256), 0, s, t, meta,
+                     tab, out, (int)S, (int)KS);
   return (int)hipGetLastError();
 }
 

@@ -341,7 +341,7 @@ int cadence_vit_features(const float* resid, void* out, int64_t ldo,
  * 148-151; both encoders' transforms share it), i.e. Pillow's
  * ImagingResample (libImaging/Resample.c) bit for bit, for a ragged batch:
  *   images  packed uint8 HWC RGB, images_bytes long; meta[b] = {byte offset,
- *           H, W, tmp offset}; every W <= max_w <= 10912, S <= 10912;
+ *           H, W, tmp offset}; max_h / max_w bound every H / W;
  *           images, coef and tmp 16-byte aligned
  *   KS      taps per coefficient row, a multiple of 4 >= 2 * ceil(2 *
  *           max(in / S, 1)) + 1 over every image side (host computes it)

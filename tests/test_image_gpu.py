@@ -35,7 +35,7 @@ def _images(rng, shapes):
 def test_resize_ragged_batch_bitexact(dev, size):
   rng = np.random.default_rng(size)
   shapes = [(480, 640), (100, 150), (size, size), (1, 7), (2217, 1353),
-            (50, 2000), (333, 517), (7, 1)]
+            (50, 2000), (333, 517), (7, 1), (3, 6000)]   # > 5450 wide: unstaged rows
   imgs = _images(rng, shapes)
   got = image_io.resize_arrays(imgs, size, dev).cpu()
   assert got.shape == (len(imgs), 3, size, size)
@@ -56,8 +56,7 @@ def test_resize_rejects_bad_input(dev):
     image_io.resize_arrays([np.zeros((4, 4), np.uint8)], 224, dev)
   with pytest.raises(ValueError):
     image_io.resize_arrays([], 224, dev)
-  with pytest.raises(RuntimeError):     # wider than one LDS-staged row
-    image_io.resize_arrays([np.zeros((2, 11000, 3), np.uint8)], 224, dev)
+
 
 
 def test_img_path_list_feeds_the_model(dev, tmp_path):
