@@ -169,11 +169,21 @@ def vit_attention_isolated(vis, batch, dev, reps=20):
     us = s.elapsed_time(e) / reps * 1e3
     flops = 4.0 * batch * c.num_heads * n * n * c.head_dim
     tf = flops / (us * 1e-6) / 1e12
+    # q|k|v read once + output written once: at bs=32 these bytes take
+    # longer at HBM peak than the FLOPs at MFMA peak, which caps the MFMA
+    # fraction any kernel of this shape can reach (mfma_frac_ceiling)
+    nbytes = batch * n * (3 * c.width + c.width) * 2
+    t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
+    t_mfma = flops / (MFMA_BF16_PEAK_TFS * 1e12)
     out[c.name] = {"kernel": f"vit_attn_kernel<hd{c.head_dim}>", "bound": "mfma",
                    "achieved": round(tf, 2), "peak": MFMA_BF16_PEAK_TFS,
                    "unit": "TFLOP/s", "frac": round(tf / MFMA_BF16_PEAK_TFS, 4),
                    "avg_us": round(us, 2), "work_per_launch": flops,
                    "shape": f"B={batch} N={n} H={c.num_heads} hd={c.head_dim}",
+                   "hbm_bytes": nbytes,
+                   "hbm_achieved": round(nbytes / (us * 1e-6) / 1e9, 1),
+                   "hbm_frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                   "mfma_frac_ceiling": round(t_mfma / max(t_mfma, t_hbm), 4),
                    "timing": f"isolated, {reps} launches after the timed region"}
   return out
 
