@@ -119,7 +119,13 @@ class LocalAttentionBlock(nn.Module):
       q, k, v = ops.ops.rope_qkv(qkv, pos.view(-1), h, hd,
                                  ops.rope_table(qkv.device, hd))
     if cache is None:
-      seg, start = ops.ops.segment_info(pos)
+      # every attention block of a forward sees the same positions tensor:
+      # its segment ids / starts are computed once and kept on it
+      info = getattr(pos, "_cadence_segment_info", None)
+      if info is None:
+        info = ops.ops.segment_info(pos)
+        pos._cadence_segment_info = info
+      seg, start = info
       enc = ops.ops.local_attention(q, k, v, seg, start, b, t, h, hd,
                                     self.window_size)
       new_cache = None

@@ -211,15 +211,39 @@ __global__ void splice_positions_kernel(const int32_t* __restrict__ text,
 }
 
 // seg_id = cumsum(pos == 0) (modules.py:145); seg_start = first index of
-// the row's segment.  One thread per sequence (L is at most a few thousand).
-__global__ void segment_info_kernel(const int32_t* __restrict__ pos,
-                                    int32_t* __restrict__ seg,
-                                    int32_t* __restrict__ start, int B, int L) {
-  const int b = blockIdx.x * 64 + threadIdx.x;
-  if (b >= B) return;
-  int s = 0, st = 0;
-  for (int t = 0; t < L; ++t) {
-    if (pos[(int64_t)b * L + t] == 0) {
+// the row's segment (0 before the first reset).  One workgroup per sequence:
+// each thread counts the resets of a contiguous slice, a block-wide
+// Hillis-Steele scan gives every slice its running count and last reset
+// index, then each thread writes its slice.
+__global__ __launch_bounds__(256) void segment_info_kernel(
+    const int32_t* __restrict__ pos, int32_t* __restrict__ seg,
+    int32_t* __restrict__ start, int B, int L) {
+  __shared__ int sc[256], sl[256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int per = (L + 255) / 256;
+  const int t0 = min(L, tid * per), t1 = min(L, t0 + per);
+  const int32_t* p = pos + (int64_t)b * L;
+  int cnt = 0, last = -1;
+  for (int t = t0; t < t1; ++t)
+    if (p[t] == 0) {
+      ++cnt;
+      last = t;
+    }
+  sc[tid] = cnt;
+  sl[tid] = last;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {
+    const int c = tid >= d ? sc[tid - d] : 0;
+    const int l = tid >= d ? sl[tid - d] : -1;
+    __syncthreads();
+    sc[tid] += c;
+    sl[tid] = max(sl[tid], l);
+    __syncthreads();
+  }
+  int s = tid ? sc[tid - 1] : 0;
+  int st = tid ? max(sl[tid - 1], 0) : 0;
+  for (int t = t0; t < t1; ++t) {
+    if (p[t] == 0) {
       ++s;
       st = t;
     }
@@ -335,8 +359,8 @@ int cadence_segment_info(const int32_t* segment_pos, int32_t* seg_id,
                          int32_t* seg_start, int64_t B, int64_t L,
                          void* stream) {
   if (B <= 0 || L <= 0) return 0;
-  hipLaunchKernelGGL(segment_info_kernel, dim3((unsigned)((B + 63) / 64)),
-                     dim3(64), 0, static_cast<hipStream_t>(stream), segment_pos,
+  hipLaunchKernelGGL(segment_info_kernel, dim3((unsigned)B),
+                     dim3(256), 0, static_cast<hipStream_t>(stream), segment_pos,
                      seg_id, seg_start, (int)B, (int)L);
   return (int)hipGetLastError();
 }

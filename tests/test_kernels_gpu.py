@@ -464,3 +464,21 @@ def test_sequence_parallel_scan_chunks_on_gpu(dev):
   assert (y == y_ref).float().mean().item() > 0.99
   torch.testing.assert_close(y.float(), y_ref.float(), rtol=1e-2, atol=1e-2)
   torch.testing.assert_close(hs[-1], h_ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("b,l", [(3, 7), (4, 319), (2, 3001)])
+def test_segment_info(dev, b, l):
+  """seg = cumsum(pos == 0) (modules.py:145) and the start index of each
+  row's segment (0 before the first reset), incl. left pads (-1)."""
+  g = torch.Generator().manual_seed(b * l)
+  pos = torch.randint(1, 50, (b, l), generator=g, dtype=torch.int32)
+  pos[torch.rand(b, l, generator=g) < 0.02] = 0
+  pos[0, :min(3, l)] = -1                   # left padding, no reset yet
+  pos[-1, 0] = 0
+  seg, start = ops.ops.segment_info(pos.to(dev))
+  want_seg = torch.cumsum((pos == 0).to(torch.int32), 1)
+  idx = torch.arange(l)[None].expand(b, l)
+  last = torch.where(pos == 0, idx, torch.zeros_like(idx))
+  want_start = torch.cummax(last, 1).values
+  assert torch.equal(seg.cpu(), want_seg.to(torch.int32))
+  assert torch.equal(start.cpu(), want_start.to(torch.int32))
