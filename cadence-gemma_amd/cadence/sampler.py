@@ -25,6 +25,7 @@ from typing import Generic, NamedTuple, Sequence, TypeVar
 import torch
 
 from . import common, ops
+from .modules import AttentionBlockCache
 
 Cache = TypeVar("Cache")
 
@@ -113,7 +114,16 @@ class Sampler:
     """
     dev = self.device
     b, t = tokens.shape
-    positions = prompt_positions(input_lengths.cpu(), t).to(dev)
+    pos_cpu = prompt_positions(input_lengths.cpu(), t)
+    positions = pos_cpu.to(dev)
+    # image tokens spliced in front by the prefill (griffin.py:179: only when
+    # the prompt holds a position 0); known on the host, so the decode graph
+    # copies only the attention-cache slots the prefill wrote
+    n_img = 0
+    model_vis = getattr(self.model, "vision_config", None)
+    if (images is not None or img_path) and model_vis is not None and bool(
+        (pos_cpu[:, :-1] == 0).any() if t > 1 else (pos_cpu == 0).any()):
+      n_img = self.model.n_visual_tokens
     tokens = tokens.to(dev, torch.int32)
     steps = total_generation_steps
     if steps == 0:
@@ -147,7 +157,8 @@ class Sampler:
         step = torch.zeros(1, dtype=torch.int32, device=dev)
         cur = tokens[:, -1].to(torch.int32).contiguous()
         self._decode_graph(cur, pos, cache, buf, step, steps,
-                           end_sampling_at_eos_token, events, start=0)
+                           end_sampling_at_eos_token, events, start=0,
+                           cache_len=n_img + t - 1)
         if echo:
           buf = torch.cat([tokens, buf], dim=1)
         return SamplingState(buf, step, torch.tensor(steps), pos[:, None], cache,
@@ -178,7 +189,8 @@ class Sampler:
                  and n_more > 1)
     if graphable:
       self._decode_graph(cur, pos, cache, buf, step, n_more,
-                         end_sampling_at_eos_token, events)
+                         end_sampling_at_eos_token, events,
+                         cache_len=n_img + t)
     else:
       for i in range(n_more):
         nxt, logits, cache = model.next_token(cur[:, None], pos[:, None], cache,
@@ -213,7 +225,7 @@ class Sampler:
     return bool((buf == self.vocab.eos_id()).any(dim=1).all())
 
   def _decode_graph(self, cur, pos, cache, buf, step, n_more, eos_stop,
-                    events=None, start=1):
+                    events=None, start=1, cache_len=None):
     """Replays a captured single-token decode step `n_more` times."""
     key = (cur.shape[0], cur.device)
     eng = self._graphs.get(key) if hasattr(self, "_graphs") else None
@@ -224,7 +236,8 @@ class Sampler:
                          cur.device)
       self._graphs[key] = eng
     eng.run(cache, cur, pos, buf, step, n_more,
-            (lambda b: self._all_done(b)) if eos_stop else None, events, start)
+            (lambda b: self._all_done(b)) if eos_stop else None, events, start,
+            cache_len)
 
   # ------------------------------------------------------------------- API
 
@@ -289,14 +302,27 @@ class _DecodeGraph:
                                       self.cache, False, inplace=True)
     ops.ops.decode_advance_(nxt, self.buf, self.step, self.pos, self.cur)
 
+  @staticmethod
+  def _copy_cache(dst_cache, src_cache, slots):
+    """Copies block caches; of the attention ring buffers only the first
+    `slots` slots (the ones written so far; decode attention never reads a
+    slot at or past num_tokens before the ring wraps), all when None."""
+    for name, src in src_cache.items():
+      dst = dst_cache[name]
+      ring = isinstance(src, AttentionBlockCache) and slots is not None
+      for d, s_ in zip(dst, src):
+        if ring and d.dim() == 4 and slots < d.shape[1]:
+          d[:, :slots].copy_(s_[:, :slots])
+        else:
+          d.copy_(s_)
+
   def run(self, cache, cur, pos, buf, step, n_more, all_done=None, events=None,
-          start=1):
+          start=1, cache_len=None):
     """Replays the step `n_more` times from buffer column `start` (the
-    tokens before it are already in `buf`)."""
+    tokens before it are already in `buf`).  `cache_len`: tokens already in
+    the attention caches (host-known), so only written ring slots move."""
     dev_stream = torch.cuda.current_stream(cur.device)
-    for name, c in cache.items():
-      for dst, src in zip(self.cache[name], c):
-        dst.copy_(src)
+    self._copy_cache(self.cache, cache, cache_len)
     self.cur.copy_(cur)
     self.pos.copy_(pos)
     self.step.fill_(start)
@@ -307,8 +333,10 @@ class _DecodeGraph:
         events["decode_end"] = torch.cuda.Event(enable_timing=True)
         events["decode_steps"] = n_more
         events["decode_start"].record()
+      done = 0
       for i in range(n_more):
         self.graph.replay()
+        done += 1
         if all_done is not None and (i % 8 == 7) and all_done(
             self.buf[:, :buf.shape[1]]):
           break
@@ -320,6 +348,5 @@ class _DecodeGraph:
     step.copy_(self.step)
     pos.copy_(self.pos)
     cur.copy_(self.cur)
-    for name, c in cache.items():
-      for dst, src in zip(c, self.cache[name]):
-        dst.copy_(src)
+    self._copy_cache(cache, self.cache,
+                     None if cache_len is None else cache_len + done)

@@ -240,3 +240,30 @@ def test_sampler_left_padded_prompts_match_oracle(dev):
   assert cosine(got_logits[:, 0], want_logits[:, 0]) > 0.999
   agree = (st.tokens_buffer.cpu().long() == want_tok).float().mean().item()
   assert agree >= 0.75, agree
+
+
+def test_decode_graph_reuse_partial_cache_copies(dev):
+  """The decode graph's static caches take only the written ring slots in
+  and out; a second generate on the same graph (stale slots from the first
+  call past num_tokens) must still equal eager decoding, tokens and caches."""
+  cfg = small_config(window=2048)
+  m, _ = make_model(dev, cfg, seed=8)
+  vocab = MockVocab()
+  graph_s = cadence.Sampler(m, vocab, use_graph=True)
+  for t, seed in ((30, 1), (12, 2)):
+    g = torch.Generator().manual_seed(seed)
+    tok = torch.randint(3, cfg.vocab_size, (4, t), generator=g, dtype=torch.int32)
+    lens = torch.full((4,), t, dtype=torch.int32)
+    eager = cadence.Sampler(m, vocab, use_graph=False).generate(tok, lens, 10)
+    graph = graph_s.generate(tok, lens, 10)
+    assert torch.equal(eager.tokens_buffer.cpu(), graph.tokens_buffer.cpu())
+    for name, ce in eager.cache.items():
+      cg = graph.cache[name]
+      if isinstance(ce, cadence.AttentionBlockCache):
+        n = int(ce.num_tokens.max())
+        assert torch.equal(ce.num_tokens, cg.num_tokens)
+        assert torch.equal(ce.keys[:, :n], cg.keys[:, :n])
+        assert torch.equal(ce.values[:, :n], cg.values[:, :n])
+      else:
+        for a, b in zip(ce, cg):
+          assert torch.equal(a, b), name
