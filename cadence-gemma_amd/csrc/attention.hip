@@ -104,31 +104,55 @@ __global__ __launch_bounds__(256) void flash_attn_kernel(AttnArgs a) {
     kend = qlast + 1;
   }
   const int rowq0 = qw + 4 * (lane >> 4);  // + r
-  int segq[4];
+  // same segment and causal <=> seg_start(q) <= key <= q (segments are
+  // contiguous runs of seg = cumsum(pos == 0)): one start per query row,
+  // no per-key segment loads in the tile loop
+  int sstart[4];
   if (MODE == MODE_LOCAL) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int qi = min(rowq0 + r, a.L - 1);
-      segq[r] = a.seg[(int64_t)b * a.L + qi];
+      sstart[r] = a.seg_start[(int64_t)b * a.L + qi];
     }
   }
 
-  for (int k0 = kbeg; k0 < kend; k0 += KT) {
-    __syncthreads();  // previous tile fully consumed
-    // stage K tile (swizzled) and V^T tile
-    for (int c = tid; c < KT * CPR; c += 256) {
+  // K / V tile staging: all of this thread's chunks of a tile are loaded
+  // (unconditional loads from clamped rows, masked after the load) before
+  // the first LDS store -- one memory round trip per tile.  (Prefetching
+  // the next tile across the compute kept 32 more VGPRs live and halved the
+  // occupancy: 193 -> 238 us.)
+  constexpr int NIT = (KT * CPR + 255) / 256;
+  uint4 kreg[NIT], vreg[NIT];
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int c = tid + i * 256;
       const int kr = c / CPR, ch = c % CPR;
       const int key = k0 + kr;
-      const int d = ch * 8;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-      if (key < a.L && d < a.hd) {
-        kv = ld16(kb + (int64_t)key * a.k_rs + d);
-        vv = ld16(vb + (int64_t)key * a.v_rs + d);
-      }
-      sm.k[kr * CPR + swz<CPR>(ch, kr)] = kv;
-      const u16* vs = reinterpret_cast<const u16*>(&vv);
+      const int kc = min(key, a.L - 1), d = min(ch * 8, a.hd - 8);
+      const uint4 kv = ld16(kb + (int64_t)kc * a.k_rs + d);
+      const uint4 vv = ld16(vb + (int64_t)kc * a.v_rs + d);
+      const uint32_t mk = (key < a.L && ch * 8 < a.hd && c < KT * CPR) ? 0xffffffffu : 0u;
+      kreg[i] = make_uint4(kv.x & mk, kv.y & mk, kv.z & mk, kv.w & mk);
+      vreg[i] = make_uint4(vv.x & mk, vv.y & mk, vv.z & mk, vv.w & mk);
+    }
+  };
+  for (int k0 = kbeg; k0 < kend; k0 += KT) {
+    load_tile(k0);
+    __syncthreads();  // previous tile fully consumed
+    // store the staged K tile (swizzled) and V^T tile
 #pragma unroll
-      for (int i = 0; i < 8; ++i) sm.vt[(d + i) * KT + kr] = vs[i];
+    for (int i = 0; i < NIT; ++i) {
+      const int c = tid + i * 256;
+      if (c < KT * CPR) {
+        const int kr = c / CPR, ch = c % CPR;
+        const int d = ch * 8;
+        sm.k[kr * CPR + swz<CPR>(ch, kr)] = kreg[i];
+        const uint4 vv = vreg[i];
+        const u16* vs = reinterpret_cast<const u16*>(&vv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sm.vt[(d + e) * KT + kr] = vs[e];
+      }
     }
     __syncthreads();
 
@@ -160,8 +184,7 @@ __global__ __launch_bounds__(256) void flash_attn_kernel(AttnArgs a) {
         if (MODE == MODE_LOCAL) {
           v = rbf(s[jn][r]) * a.scale;
           const int qi = rowq0 + r;
-          ok = key < a.L && key <= qi && qi <= key + a.window &&
-               a.seg[(int64_t)b * a.L + min(key, a.L - 1)] == segq[r];
+          ok = key < a.L && key <= qi && qi <= key + a.window && key >= sstart[r];
         } else {
           v = s[jn][r] * a.scale;
           ok = key < a.L;
