@@ -79,6 +79,72 @@ __global__ __launch_bounds__(256) void conv1d_prefill_kernel(
   }
 }
 
+// Same arithmetic for a compile-time width: every load of the thread (TW
+// input rows from clamped time indices, TW weight rows, the bias, the TW-1
+// positions the document mask reads) is issued before the first multiply,
+// instead of one dependent round trip per tap; terms accumulate in the same
+// order (s = 0 .. TW-1, then + bias) with the same bf16 rounding.
+template <int TW>
+__global__ __launch_bounds__(256) void conv1d_prefill_tw_kernel(
+    const u16* __restrict__ x, int64_t ldx, const u16* __restrict__ w,
+    const u16* __restrict__ bias, const int32_t* __restrict__ pos,
+    u16* __restrict__ out, int64_t ldo, u16* __restrict__ cache_out, int B,
+    int L, int E, int compat) {
+  const int ch8 = E / 8;
+  const int64_t total = (int64_t)B * L * ch8;
+  for (int64_t idx = blockIdx.x * 256 + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * 256) {
+    const int c = idx % ch8;
+    const int64_t bt = idx / ch8;
+    const int t = bt % L, b = bt / L;
+    const int e0 = c * 8;
+    const int64_t row0 = (int64_t)b * L;
+    uint4 xr[TW], wr[TW];
+    bool nz[TW > 1 ? TW - 1 : 1];
+#pragma unroll
+    for (int s = 0; s < TW; ++s) {
+      xr[s] = ld16(x + (row0 + max(t - s, 0)) * ldx + e0);
+      wr[s] = ld16(w + (int64_t)(TW - 1 - s) * E + e0);
+    }
+#pragma unroll
+    for (int j = 0; j + 1 < TW; ++j) nz[j] = pos[row0 + max(t - j, 0)] != 0;
+    const uint4 br = ld16(bias + e0);
+    float acc[8];
+#pragma unroll
+    for (int s = 0; s < TW; ++s) {
+      if (s >= L) break;   // taps past the sequence are skipped, not added as 0
+      // document mask: pos[t - s + k] != 0 for k = 1..look, i.e. nz[s - k]
+      const int look = compat ? s - 2 : s;
+      bool keep = t - s >= 0;
+#pragma unroll
+      for (int k = 1; k <= TW; ++k)
+        if (k <= look) keep = keep && nz[s - k];
+      float xv[8], wv[8];
+      unpack8(xr[s], xv);
+      unpack8(wr[s], wv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float term = bmul(keep ? xv[i] : 0.0f, wv[i]);
+        acc[i] = s == 0 ? term : badd(acc[i], term);
+      }
+    }
+    float bv[8];
+    unpack8(br, bv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = badd(acc[i], bv[i]);
+    st16(out + (row0 + t) * ldo + e0, pack8(acc));
+    if (cache_out && t >= L - (TW - 1)) {
+      const int slot = t - (L - (TW - 1));
+      st16(cache_out + ((int64_t)b * (TW - 1) + slot) * E + e0, xr[0]);
+    }
+    if (cache_out && t == 0 && L < TW - 1) {
+      for (int slot = 0; slot < TW - 1 - L; ++slot)
+        st16(cache_out + ((int64_t)b * (TW - 1) + slot) * E + e0,
+             make_uint4(0, 0, 0, 0));
+    }
+  }
+}
+
 // Single-token decode: full = [state (TW-1 rows), x]; no document mask
 // (layers.py:478-483).  cache_out may alias cache_in (each thread reads its
 // 8 channels of every state row before writing them).
@@ -466,12 +532,20 @@ int cadence_conv1d(const void* x, int64_t ldx, const void* w, const void* b,
 #undef CADENCE_CONV_TW
     }
   } else {
-    hipLaunchKernelGGL(conv1d_prefill_kernel, dim3(grid_for(B * L * E / 8)),
-                       dim3(256), 0, st, static_cast<const u16*>(x), ldx,
-                       static_cast<const u16*>(w), static_cast<const u16*>(b),
-                       segment_pos, static_cast<u16*>(out), ldo,
-                       static_cast<u16*>(cache_out), (int)B, (int)L, (int)E,
-                       (int)temporal_width, compat);
+    if (temporal_width == 4)
+      hipLaunchKernelGGL(conv1d_prefill_tw_kernel<4>, dim3(grid_for(B * L * E / 8)),
+                         dim3(256), 0, st, static_cast<const u16*>(x), ldx,
+                         static_cast<const u16*>(w), static_cast<const u16*>(b),
+                         segment_pos, static_cast<u16*>(out), ldo,
+                         static_cast<u16*>(cache_out), (int)B, (int)L, (int)E,
+                         compat);
+    else
+      hipLaunchKernelGGL(conv1d_prefill_kernel, dim3(grid_for(B * L * E / 8)),
+                         dim3(256), 0, st, static_cast<const u16*>(x), ldx,
+                         static_cast<const u16*>(w), static_cast<const u16*>(b),
+                         segment_pos, static_cast<u16*>(out), ldo,
+                         static_cast<u16*>(cache_out), (int)B, (int)L, (int)E,
+                         (int)temporal_width, compat);
   }
   return (int)hipGetLastError();
 }
