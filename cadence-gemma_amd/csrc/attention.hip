@@ -594,10 +594,20 @@ __global__ __launch_bounds__(256) void rope_qkv_kernel(
     const u16* src = qkv + m * ld + hh * hd;
     u16* dst = hh < H ? qo + m * (int64_t)H * hd + hh * hd : ko + m * hd;
     const int i0 = c * 8;
-    float x1[8], x2[8];
-    unpack8(ld16(src + i0), x1);
-    unpack8(ld16(src + quarter + i0), x2);
+    // every load independent of the position issued first: the rotated
+    // pair, this thread's 16 pass-through dims (hd / 2 / cpq == 16 for
+    // every hd) and, for the K head, its 32 dims of V (hd / cpq == 32)
     const int p = pos[m];
+    const uint4 r1 = ld16(src + i0), r2 = ld16(src + quarter + i0);
+    const int pt0 = half + c * 16;
+    const uint4 pt[2] = {ld16(src + pt0), ld16(src + pt0 + 8)};
+    uint4 vv[4];
+    const u16* vs = qkv + m * ld + (H + 1) * hd + c * 32;
+    if (hh == H) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) vv[j] = ld16(vs + 8 * j);
+    }
+    float x1[8], x2[8];
     float sn[8], cs[8];
     if (p >= 0 && p < table_len) {
       unpack8(ld16(table + ((int64_t)p * 2) * quarter + i0), sn);
@@ -606,6 +616,8 @@ __global__ __launch_bounds__(256) void rope_qkv_kernel(
 #pragma unroll
       for (int i = 0; i < 8; ++i) rope_sincos(p, i0 + i, half, sn[i], cs[i]);
     }
+    unpack8(r1, x1);
+    unpack8(r2, x2);
     float o1[8], o2[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -614,14 +626,11 @@ __global__ __launch_bounds__(256) void rope_qkv_kernel(
     }
     st16(dst + i0, pack8(o1));
     st16(dst + quarter + i0, pack8(o2));
-    // pass-through half: this thread copies dims [half + 2*i0*?..)
-    const int pt_per = (hd - half) / cpq;  // dims per thread
-    for (int d = half + c * pt_per; d < half + (c + 1) * pt_per; d += 8)
-      st16(dst + d, ld16(src + d));
+    st16(dst + pt0, pt[0]);
+    st16(dst + pt0 + 8, pt[1]);
     if (hh == H) {
-      const u16* vs = qkv + m * ld + (H + 1) * hd;
-      for (int d = c * (hd / cpq); d < (c + 1) * (hd / cpq); d += 8)
-        st16(vo + m * hd + d, ld16(vs + d));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st16(vo + m * hd + c * 32 + 8 * j, vv[j]);
     }
   }
 }
