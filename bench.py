@@ -2,15 +2,17 @@
 """CadenceGemma multimodal prefill+decode benchmark on MI355X.
 
 Metric (BASELINE.json): multimodal prefill+decode tokens/sec, Cadence-2B,
-224 px, bs=32 per GPU, 1 -> 8 MI355X.  One step = one batch through the
-whole hot path: dual ViT (DINOv2-L/14-reg4 + SigLIP-so400m/14, 23 blocks
-each) -> projector -> Griffin-2B prefill on [image | prompt[:-1]] -> cached
-step on the last prompt token -> 31 greedy decode steps (hipGraph replay)
--> one all-gather of the generated tokens (RCCL on N > 1).
-Tokens per step per GPU = B * (n_vis + prompt + decode) = 32 * (256+64+32).
+224 px, bs=32, 1 -> 8 MI355X.  One step = the global batch of 256 (image,
+prompt) samples (strong scaling, k GPUs each run 256 / (32 k)
+micro-batches of 32) through the whole hot path: dual ViT (DINOv2-L/14-reg4
++ SigLIP-so400m/14, 23 blocks each) -> projector -> Griffin-2B prefill on
+[image | prompt[:-1]] -> cached step on the last prompt token -> 31 greedy
+decode steps (hipGraph replay) per micro-batch, then one all-gather of the
+generated tokens (RCCL on N > 1).  Tokens per step = 256 * (256+64+32).
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
+  python bench.py --config c2|c3|c4                      (the other configs)
 
 Prints ONE JSON line on rank 0 (see the driver contract in the task).
 """
@@ -52,21 +54,46 @@ class BenchVocab:
     return 1
 
 
+# SURVEY §8d configurations (BASELINE.json configs 2-4); the default is the
+# metric's workload (C5 shape at 224 px: global batch 256, micro-batch 32).
+CONFIGS = {
+    "bench": dict(image_size=224, batch=32, global_batch=256, prompt=64,
+                  decode=32, text_only=False),
+    "c2": dict(image_size=224, batch=32, global_batch=0, prompt=2048,
+               decode=64, text_only=True),
+    "c3": dict(image_size=224, batch=1, global_batch=0, prompt=64, decode=32,
+               text_only=False),
+    "c4": dict(image_size=336, batch=32, global_batch=0, prompt=64, decode=0,
+               text_only=False),
+}
+
+
 def parse():
   ap = argparse.ArgumentParser()
   ap.add_argument("--gpus", type=int, default=1)
   ap.add_argument("--steps", type=int, default=5)
   ap.add_argument("--warmup", type=int, default=2)
-  ap.add_argument("--batch", type=int, default=32, help="samples per GPU")
-  ap.add_argument("--image-size", type=int, default=224)
-  ap.add_argument("--prompt", type=int, default=64)
-  ap.add_argument("--decode", type=int, default=32)
+  ap.add_argument("--config", choices=sorted(CONFIGS), default="bench")
+  ap.add_argument("--batch", type=int, help="micro-batch (samples per launch "
+                  "chain on one GPU)")
+  ap.add_argument("--global-batch", type=int,
+                  help="samples per step over all ranks (strong scaling); 0 = "
+                  "batch x world (weak scaling)")
+  ap.add_argument("--image-size", type=int)
+  ap.add_argument("--prompt", type=int)
+  ap.add_argument("--decode", type=int)
   ap.add_argument("--no-cpu-baseline", action="store_true")
-  ap.add_argument("--cpu-decode-steps", type=int, default=32)
+  ap.add_argument("--cpu-decode-steps", type=int)
   ap.add_argument("--no-kernel-timing", action="store_true")
-  ap.add_argument("--text-only", action="store_true",
+  ap.add_argument("--text-only", action="store_true", default=None,
                   help="C2-style text-only run (no vision tower)")
-  return ap.parse_args()
+  args = ap.parse_args()
+  for k, v in CONFIGS[args.config].items():
+    if getattr(args, k) is None:
+      setattr(args, k, v)
+  if args.cpu_decode_steps is None:
+    args.cpu_decode_steps = args.decode
+  return args
 
 
 def build_model(dev, image_size, text_only):
@@ -80,18 +107,44 @@ def build_model(dev, image_size, text_only):
 
 
 def make_inputs(global_batch, lo, hi, image_size, prompt, vocab, text_only):
+  """Rank-local slice [lo, hi) of the global synthetic batch: prompt tokens
+  from one seeded stream over the whole batch (so every rank agrees), the
+  images generated per rank from a seed of its first sample."""
   g = torch.Generator().manual_seed(4321)
   tok = torch.randint(3, vocab, (global_batch, prompt), generator=g,
                       dtype=torch.int32)
   tok[:, 0] = BenchVocab().bos_id()
   images = None
   if not text_only:
-    gi = torch.Generator().manual_seed(1234)
-    # generated per-rank slice of the same global stream (no 8x host copy)
-    per = hi - lo
-    gi.manual_seed(1234 + lo)
-    images = torch.rand(per, 3, image_size, image_size, generator=gi)
+    # one seeded stream per global sample index: any sharding of the batch
+    # over any number of ranks sees the same images
+    images = torch.empty(hi - lo, 3, image_size, image_size)
+    for i in range(lo, hi):
+      gi = torch.Generator().manual_seed(1234 + i)
+      images[i - lo] = torch.rand(3, image_size, image_size, generator=gi)
   return tok[lo:hi].contiguous(), images
+
+
+def shard_plan(global_batch, micro_batch, rank, world):
+  """(lo, hi, micro-batch slices) of the samples `rank` runs: a contiguous
+  block of the global batch, cut into micro-batches of `micro_batch`."""
+  lo, hi = D.shard_range(global_batch, rank, world)
+  if (hi - lo) % micro_batch:
+    raise ValueError(f"{hi - lo} samples per rank is not a multiple of the "
+                     f"micro-batch {micro_batch}")
+  n = (hi - lo) // micro_batch
+  return lo, hi, [slice(j * micro_batch, (j + 1) * micro_batch) for j in range(n)]
+
+
+def cpu_model_name():
+  try:
+    with open("/proc/cpuinfo") as f:
+      for line in f:
+        if line.startswith("model name"):
+          return line.split(":", 1)[1].strip()
+  except OSError:
+    pass
+  return None
 
 
 def pmc_traffic(key):
@@ -235,6 +288,8 @@ def cpu_baseline(model, cfg, vis, tokens, images, decode_steps):
   cores, on a bounded sample: 1 sample, full image + prompt prefill,
   `decode_steps` greedy decode steps."""
   from oracle import griffin_ref as R
+  # the host cores this process may use, capped by the box's CPU share
+  # (OMP_NUM_THREADS = 16 per GPU there: sched_getaffinity sees the machine)
   cores = min(len(os.sched_getaffinity(0)), int(os.environ.get(
       "OMP_NUM_THREADS", "16") or 16))
   torch.set_num_threads(cores)
@@ -247,8 +302,9 @@ def cpu_baseline(model, cfg, vis, tokens, images, decode_steps):
   n_vis = 0 if vis is None else vis.n_visual_tokens
   ntok = n_vis + tok.shape[1] + decode_steps
   return {"value": round(ntok / dt, 2), "unit": "tokens/s", "cores": cores,
-          "kind": "port",
-          "sample": (f"1 sample (B=1, the reference cannot batch): "
+          "kind": "port", "cpu_model": cpu_model_name(),
+          "sample": (f"1 sample (B=1, the reference cannot batch; one sample "
+                     f"keeps the leg within the harness's 10-30 s bound): "
                      f"{n_vis} image + {tok.shape[1]} prompt tokens prefill + "
                      f"{decode_steps} decode steps, {dt:.1f} s"),
           "seconds": round(dt, 2)}
@@ -263,8 +319,10 @@ def main():
   torch.cuda.set_device(dev)
   cfg, vis, model = build_model(dev, args.image_size, args.text_only)
   n_vis = 0 if vis is None else vis.n_visual_tokens
-  gb = args.batch * world
-  lo, hi = D.shard_range(gb, rank, world)
+  strong = bool(args.global_batch)
+  gb = args.global_batch if strong else args.batch * world
+  lo, hi, micro = shard_plan(gb, args.batch, rank, world)
+  n_micro = len(micro)
   tok_cpu, img_cpu = make_inputs(gb, lo, hi, args.image_size, args.prompt,
                                  cfg.vocab_size, args.text_only)
   tokens = tok_cpu.to(dev)
@@ -273,33 +331,50 @@ def main():
   sampler = cadence.Sampler(model, BenchVocab(), use_graph=True)
 
   def step(events=None):
-    st = sampler.generate(tokens, lengths, args.decode, images=images,
-                          events=events)
-    return D.gather_rows(st.tokens_buffer)
+    outs = []
+    for j, sl in enumerate(micro):
+      ev = events if j == 0 else None
+      if args.decode == 0 and ev is not None:    # prefill only (C4)
+        ev["prefill_start"] = torch.cuda.Event(enable_timing=True)
+        ev["prefill_end"] = torch.cuda.Event(enable_timing=True)
+        ev["prefill_start"].record()
+      st = sampler.generate(tokens[sl], lengths, args.decode,
+                            images=None if images is None else images[sl],
+                            events=ev)
+      if args.decode == 0 and ev is not None:
+        ev["prefill_end"].record()
+      outs.append(st.tokens_buffer)
+    return D.gather_rows(torch.cat(outs))
 
   with torch.no_grad():
     for _ in range(args.warmup):
       out = step()
     torch.cuda.synchronize()
     D.barrier()
-    # ~400 timed launches per step; a seeded 1/4 of them carry events
-    ops.TIMER.reset(pool=0 if args.no_kernel_timing else 250 * args.steps,
-                    sample=4)
+    # ~400 timed launches per micro-batch; a seeded 1/4 of them carry events
+    ops.TIMER.reset(pool=0 if args.no_kernel_timing else
+                    250 * args.steps * n_micro, sample=4)
     ops.TIMER.enabled = not args.no_kernel_timing
     prefill_ms = []
     ev_list = []
+    step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    step_ev[0].record()
+    for i in range(args.steps):
       ev = {}
       out = step(ev)
+      step_ev[i + 1].record()
       ev_list.append(ev)
     torch.cuda.synchronize()
     D.barrier()
     t1 = time.perf_counter()
     ops.TIMER.enabled = False
   elapsed = D.max_over_ranks(t1 - t0)
+  per_step = sorted(step_ev[i].elapsed_time(step_ev[i + 1])
+                    for i in range(args.steps))
+  median_ms = D.max_over_ranks(per_step[len(per_step) // 2])
   decode_ms = []
   for ev in ev_list:
     prefill_ms.append(ev["prefill_start"].elapsed_time(ev["prefill_end"]))
@@ -317,7 +392,8 @@ def main():
   ms_step = elapsed / args.steps * 1e3
   pre_ms = sum(prefill_ms) / max(len(prefill_ms), 1)
   pre_ms = D.max_over_ranks(pre_ms)
-  prefill_tps = gb * (n_vis + args.prompt - 1) / (pre_ms * 1e-3)
+  prefill_tps = args.batch * (n_vis + args.prompt - (1 if args.decode else 0)) / (
+      pre_ms * 1e-3)
 
   result = None
   if rank == 0:
@@ -340,29 +416,37 @@ def main():
              "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
              "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
              "avg_us": round(us, 1), "work_per_launch": nbytes}
+    what = ("text-only" if args.text_only else f"{args.image_size}px")
+    metric = METRIC if args.config == "bench" else (
+        f"{'text-only' if args.text_only else 'multimodal'} prefill"
+        f"{'+decode' if args.decode else ''} tokens/sec, Cadence-2B {what} "
+        f"bs={args.batch} (SURVEY §8d {args.config.upper()})")
     result = {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(value, 2),
         "unit": "tokens/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
+        "ms_per_step_median": round(median_ms, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": ("synthetic: torch.rand images (seed 1234), random prompt "
-                 "tokens (seed 4321), random-init weights (seed 0)"),
+        "data": ("synthetic: torch.rand images (seeded per sample), random "
+                 "prompt tokens (seed 4321), random-init weights (seed 0)"),
         "config": {
             "workload": ("Cadence-2B (RecurrentGemma-2B + DINOv2-L/14-reg4 + "
-                         "SigLIP-so400m/14 + MLP projector) "
-                         + ("text-only" if args.text_only else
-                            f"{args.image_size}px") +
-                         f", bs={args.batch}/GPU, prompt {args.prompt}, "
-                         f"greedy decode {args.decode}"),
-            "global_batch": gb, "image_size": None if args.text_only
-            else args.image_size, "n_visual_tokens": n_vis,
+                         "SigLIP-so400m/14 + MLP projector) " + what +
+                         f", global batch {gb} = {world} GPU(s) x {n_micro} "
+                         f"micro-batch(es) of {args.batch}, prompt "
+                         f"{args.prompt}, greedy decode {args.decode}"),
+            "config": args.config,
+            "global_batch": gb, "micro_batch": args.batch,
+            "micro_batches_per_gpu": n_micro,
+            "image_size": None if args.text_only else args.image_size,
+            "n_visual_tokens": n_vis,
             "prompt_len": args.prompt, "decode_steps": args.decode,
             "seq_len": n_vis + args.prompt + args.decode,
             "parallelism": f"dp{world}",
@@ -375,7 +459,8 @@ def main():
         "roofline_vit_attention": vit_iso,
         "roofline_image_preprocess": img_iso,
         "roofline_by_kernel": {k: roofline_entry(ksum, k, "mfma") for k in sorted(ksum)
-                               if k.startswith(("gemm_big", "vit_attn", "flash_attn"))},
+                               if k.startswith(("gemm_big", "vit_attn", "flash_attn",
+                                                "griffin_attn"))},
         # a seeded 1/sample of the launches is event-timed (TIMER.sample)
         "kernels": {k: {"launches_timed": v["launches"],
                         "avg_us": round(v["avg_ms"] * 1e3, 2),

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -59,7 +59,8 @@ _SIGS: dict[str, list] = {
     "cadence_conv1d": [P, I64, P, P, P, P, P, I64, P, I64, I64, I64, I64, I32,
                        P],
     "cadence_rnn_scan": [P, I64, P, I64, P, P, P, I64, P, I64, P, I64, I64, I64,
-                         P],
+                         P, I64, P],
+    "cadence_rnn_scan_workspace_bytes": [I64, I64, I64],
     "cadence_segment_info": [P, P, P, I64, I64, P],
     "cadence_rope_qkv": [P, I64, P, P, P, P, I64, I64, I64, P, I64, P],
     "cadence_rope_table": [P, I64, I64, P],
@@ -75,13 +76,14 @@ _SIGS: dict[str, list] = {
     "cadence_resize_bicubic": [P, I64, P, I64, I64, I64, I64, I64, P, P, I64, P,
                                P],
     "cadence_splice_positions": [P, P, I64, I64, I64, P],
-    "cadence_decode_advance": [P, P, I64, P, P, P, I64, P],
+    "cadence_decode_advance": [P, P, I64, P, P, P, P, I32, I32, I64, P],
 }
 _RESTYPE = {
     "cadence_gemm_workspace_bytes": I64,
     "cadence_local_attention_decode_workspace_bytes": I64,
     "cadence_gemm_rmsnorm_workspace_bytes": I64,
     "cadence_logits_scratch_bytes": I64,
+    "cadence_rnn_scan_workspace_bytes": I64,
 }
 
 

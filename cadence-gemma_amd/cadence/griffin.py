@@ -91,7 +91,10 @@ class Griffin(nn.Module):
     d = self.config.width
     dev = tokens.device
     pos = segment_pos.to(torch.int32).contiguous()
-    want_image = (images is not None or img_path) and self.vision_config is not None
+    if (images is not None or img_path) and self.vision_config is None:
+      raise ValueError("images / img_path were given to a Griffin built "
+                       "without a vision tower (vision=None)")
+    want_image = images is not None or bool(img_path)
     if want_image and bool((pos == 0).any()):          # griffin.py:179
       n_vis = self.n_visual_tokens
       length = n_vis + t

@@ -582,6 +582,15 @@ def _conv1d(x, w, b, segment_pos, cache, B, L, compat):
   return out, new_cache
 
 
+def _scan_workspace(B, L, E, device):
+  """Stream-ordered workspace for the chunked scan (small batches), from the
+  caching allocator; (None, 0) when the sequential kernel runs."""
+  n = _lib.load().cadence_rnn_scan_workspace_bytes(B, L, E)
+  if n <= 0:
+    return None, 0
+  return torch.empty(n, dtype=torch.uint8, device=device), n
+
+
 @_reg("rnn_scan(Tensor x, Tensor a, Tensor? segment_pos, Tensor? h0, "
       "Tensor? gate, int B, int L) -> (Tensor, Tensor)")
 def _rnn_scan(x, a, segment_pos, h0, gate, B, L):
@@ -593,10 +602,11 @@ def _rnn_scan(x, a, segment_pos, h0, gate, B, L):
   out = torch.empty(B * L, E, dtype=_BF16, device=x.device)
   h_last = torch.empty(B, E, dtype=_F32, device=x.device)
   pos = segment_pos.contiguous() if segment_pos is not None else None
+  ws, wsb = _scan_workspace(B, L, E, x.device)
   ev = TIMER.start(x) if L > 1 else None
   _lib.check(_lib.load().cadence_rnn_scan(
       _p(x), ldx, _p(a), lda, _p(pos), _p(h0), _p(gate), ldg, _p(out), E,
-      _p(h_last), B, L, E, _s(x)), "rnn_scan")
+      _p(h_last), B, L, E, _p(ws), wsb, _s(x)), "rnn_scan")
   # algorithmic bytes: x, a (+ gate) in and y out as bf16 per element,
   # fp32 state out (+ in), int32 reset per token when given
   per_elem = 6 + (2 if gate is not None else 0)
@@ -630,9 +640,10 @@ def _rnn_scan_inplace(x, a, h, gate, B, L):
   ldg = _mat(gate, "gate") if gate is not None else 0
   _need(h.dtype == _F32 and h.is_contiguous(), "h fp32")
   out = torch.empty(B * L, E, dtype=_BF16, device=x.device)
+  ws, wsb = _scan_workspace(B, L, E, x.device)
   _lib.check(_lib.load().cadence_rnn_scan(
       _p(x), ldx, _p(a), lda, None, _p(h), _p(gate), ldg, _p(out), E, _p(h), B,
-      L, E, _s(x)), "rnn_scan_")
+      L, E, _p(ws), wsb, _s(x)), "rnn_scan_")
   return out
 
 
@@ -858,15 +869,21 @@ def _splice_positions(text_pos, n_vis):
 
 
 @_reg("decode_advance_(Tensor next_token, Tensor(a!) tokens_out, "
-      "Tensor(b!) step, Tensor(c!) positions, Tensor(d!)? cur=None) -> ()")
-def _decode_advance(next_token, tokens_out, step, positions, cur=None):
+      "Tensor(b!) step, Tensor(c!) positions, Tensor(d!)? cur=None, "
+      "Tensor(e!)? done=None, int eos_id=-1, int pad_id=0) -> ()")
+def _decode_advance(next_token, tokens_out, step, positions, cur=None,
+                    done=None, eos_id=-1, pad_id=0):
   B = next_token.numel()
   _need(tokens_out.dtype == _I32 and tokens_out.stride(1) == 1, "tokens_out")
   if cur is not None:
     _need(cur.dtype == _I32 and cur.is_contiguous() and cur.numel() == B, "cur")
+  if done is not None:
+    _need(done.dtype == _I32 and done.is_contiguous() and done.numel() == B + 1,
+          "done must be int32[B + 1]")
   _lib.check(_lib.load().cadence_decode_advance(
       _p(next_token), _p(tokens_out), tokens_out.stride(0), _p(step),
-      _p(positions), _p(cur), B, _s(next_token)), "decode_advance")
+      _p(positions), _p(cur), _p(done), int(eos_id), int(pad_id), B,
+      _s(next_token)), "decode_advance")
 
 
 # ----------------------------------------------------------------- helpers

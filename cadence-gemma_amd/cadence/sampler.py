@@ -156,15 +156,16 @@ class Sampler:
         pos = positions[:, -1].to(torch.int32).contiguous()
         step = torch.zeros(1, dtype=torch.int32, device=dev)
         cur = tokens[:, -1].to(torch.int32).contiguous()
-        self._decode_graph(cur, pos, cache, buf, step, steps,
-                           end_sampling_at_eos_token, events, start=0,
-                           cache_len=n_img + t - 1)
+        done = self._decode_graph(cur, pos, cache, buf, step, steps,
+                                  end_sampling_at_eos_token, events, start=0,
+                                  cache_len=n_img + t - 1)
         if echo:
           buf = torch.cat([tokens, buf], dim=1)
         return SamplingState(buf, step, torch.tensor(steps), pos[:, None], cache,
-                             torch.zeros(b, dtype=torch.bool), None)
+                             done, None)
       nxt, logits, cache = model.next_token(tokens[:, -1:], positions[:, -1:],
-                                            cache, return_logits)
+                                            cache, return_logits or
+                                            not self.greedy_sampling)
     else:
       logits_all, cache = self.apply_model(tokens, positions, None, True, True,
                                            img_path, images)
@@ -175,24 +176,30 @@ class Sampler:
     first_logits = logits
     buf = torch.full((b, steps), self.vocab.pad_id(), dtype=torch.int32,
                      device=dev)
-    buf[:, 0] = nxt
     lbuf = None
     if return_logits:
       lbuf = torch.zeros(b, steps, self.vocab_size, dtype=self.dtype,
                          device=dev)
       lbuf[:, 0] = logits
-    pos = (positions[:, -1] + 1).contiguous()
-    step = torch.ones(1, dtype=torch.int32, device=dev)
-    cur = nxt.to(torch.int32).contiguous()
+    # the first token goes through the same on-device bookkeeping as the
+    # rest: buf[:, 0], positions + 1, step 1, EOS flags
+    pos = positions[:, -1].to(torch.int32).contiguous()
+    step = torch.zeros(1, dtype=torch.int32, device=dev)
+    cur = torch.empty(b, dtype=torch.int32, device=dev)
+    dflags = self._done_flags(b, end_sampling_at_eos_token)
+    self._advance(nxt, buf, step, pos, cur, dflags)
     n_more = steps - 1
     graphable = (self.use_graph and self.greedy_sampling and not return_logits
                  and n_more > 1)
     if graphable:
-      self._decode_graph(cur, pos, cache, buf, step, n_more,
-                         end_sampling_at_eos_token, events,
-                         cache_len=n_img + t)
+      done = self._decode_graph(cur, pos, cache, buf, step, n_more,
+                                end_sampling_at_eos_token, events,
+                                cache_len=n_img + t, done_in=dflags)
     else:
+      watch = _DoneWatch(dflags)
       for i in range(n_more):
+        if watch.finished(i):
+          break
         nxt, logits, cache = model.next_token(cur[:, None], pos[:, None], cache,
                                               return_logits or not
                                               self.greedy_sampling)
@@ -200,10 +207,8 @@ class Sampler:
           nxt = self._sample(logits)
         if return_logits:
           lbuf[:, i + 1] = logits
-        ops.ops.decode_advance_(nxt, buf, step, pos)
-        cur.copy_(nxt)
-        if end_sampling_at_eos_token and (i % 8 == 7) and self._all_done(buf):
-          break
+        self._advance(nxt, buf, step, pos, cur, dflags)
+      done = _row_done(dflags, b, dev)
     if echo:
       buf = torch.cat([tokens, buf], dim=1)
       if return_logits:
@@ -213,7 +218,7 @@ class Sampler:
         lbuf = torch.cat([prompt_logits, first_logits[:, None].to(lbuf.dtype),
                           lbuf], dim=1)
     return SamplingState(buf, step, torch.tensor(steps), pos[:, None], cache,
-                         torch.zeros(b, dtype=torch.bool), lbuf)
+                         done, lbuf)
 
   def _sample(self, logits: torch.Tensor) -> torch.Tensor:
     if self.greedy_sampling:
@@ -221,23 +226,38 @@ class Sampler:
     return torch.distributions.Categorical(logits=logits.float()).sample().to(
         torch.int32)
 
-  def _all_done(self, buf: torch.Tensor) -> bool:
-    return bool((buf == self.vocab.eos_id()).any(dim=1).all())
+  def _done_flags(self, b, eos_stop):
+    """int32[B + 1] on-device EOS flags (row latches, all-rows flag), or None
+    when sampling does not stop at EOS."""
+    if not eos_stop:
+      return None
+    return torch.zeros(b + 1, dtype=torch.int32, device=self.device)
+
+  def _advance(self, nxt, buf, step, pos, cur, dflags):
+    ops.ops.decode_advance_(nxt, buf, step, pos, cur, dflags,
+                            int(self.vocab.eos_id()), int(self.vocab.pad_id()))
 
   def _decode_graph(self, cur, pos, cache, buf, step, n_more, eos_stop,
-                    events=None, start=1, cache_len=None):
-    """Replays a captured single-token decode step `n_more` times."""
-    key = (cur.shape[0], cur.device)
-    eng = self._graphs.get(key) if hasattr(self, "_graphs") else None
-    if eng is None or eng.max_steps < buf.shape[1]:
-      if not hasattr(self, "_graphs"):
-        self._graphs = {}
+                    events=None, start=1, cache_len=None, done_in=None):
+    """Replays a captured single-token decode step `n_more` times.
+
+    The graph holds raw pointers to the model's (packed) weights, so it is
+    keyed on the parameters' storage and version counters: a weight reload
+    or in-place update recaptures it."""
+    if not hasattr(self, "_graphs"):
+      self._graphs = {}
+    key = (cur.shape[0], cur.device, bool(eos_stop))
+    version = tuple((p.data_ptr(), p._version) for p in self.model.parameters())
+    eng = self._graphs.get(key)
+    if eng is None or eng.max_steps < buf.shape[1] or eng.version != version:
+      self._graphs.pop(key, None)
       eng = _DecodeGraph(self.model, cache, cur.shape[0], buf.shape[1],
-                         cur.device)
+                         cur.device, eos_stop,
+                         (int(self.vocab.eos_id()), int(self.vocab.pad_id())))
+      eng.version = version
       self._graphs[key] = eng
-    eng.run(cache, cur, pos, buf, step, n_more,
-            (lambda b: self._all_done(b)) if eos_stop else None, events, start,
-            cache_len)
+    return eng.run(cache, cur, pos, buf, step, n_more, events, start,
+                   cache_len, done_in)
 
   # ------------------------------------------------------------------- API
 
@@ -271,22 +291,65 @@ def _clone_cache(cache):
   return {k: type(v)(*[t.clone() for t in v]) for k, v in cache.items()}
 
 
+def _row_done(dflags, b, dev):
+  if dflags is None:
+    return torch.zeros(b, dtype=torch.bool, device=dev)
+  return dflags[:b].bool()
+
+
+class _DoneWatch:
+  """Host view of the on-device all-rows-done flag without stalling the GPU.
+
+  Every `every` steps the flag is copied (async) into pinned memory behind
+  an event; the check waits only on the copy issued one period earlier, so
+  the host stays at most two periods ahead of the GPU and the GPU queue
+  never drains.  Steps issued after the rows finished only write pad
+  (decode_advance latches per row), so stopping late changes no output.
+  """
+
+  def __init__(self, dflags, every=8):
+    self.flags = dflags
+    self.every = every
+    self.pending = []
+    if dflags is not None:
+      self.host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+
+  def finished(self, i):
+    if self.flags is None or i == 0 or i % self.every:
+      return False
+    slot = (i // self.every) % 2
+    ev = torch.cuda.Event()
+    self.host[slot:slot + 1].copy_(self.flags[-1:], non_blocking=True)
+    ev.record()
+    self.pending.append((slot, ev))
+    if len(self.pending) < 2:
+      return False
+    pslot, pev = self.pending.pop(0)
+    pev.synchronize()
+    return bool(self.host[pslot])
+
+
 class _DecodeGraph:
   """One single-token decode step captured into a hipGraph.
 
-  Static buffers: current token, positions, token buffer, step counter and a
-  private copy of every block cache (recurrent states and attention ring
-  buffers are updated in place by the kernels).  `run` copies the prefill
-  state in, replays the graph, and copies the generated tokens out.
+  Static buffers: current token, positions, token buffer, step counter, the
+  EOS flags and a private copy of every block cache (recurrent states and
+  attention ring buffers are updated in place by the kernels).  `run`
+  copies the prefill state in, replays the graph, and copies the generated
+  tokens out.
   """
 
-  def __init__(self, model, cache_like, batch, max_steps, device):
+  def __init__(self, model, cache_like, batch, max_steps, device, eos_stop,
+               eos_pad):
     self.model = model
     self.max_steps = max_steps
+    self.eos_pad = eos_pad
     self.cur = torch.zeros(batch, dtype=torch.int32, device=device)
     self.pos = torch.zeros(batch, dtype=torch.int32, device=device)
     self.buf = torch.zeros(batch, max_steps, dtype=torch.int32, device=device)
     self.step = torch.ones(1, dtype=torch.int32, device=device)
+    self.done = (torch.zeros(batch + 1, dtype=torch.int32, device=device)
+                 if eos_stop else None)
     self.cache = _clone_cache(cache_like)
     self.stream = torch.cuda.Stream(device=device)
     self.stream.wait_stream(torch.cuda.current_stream(device))
@@ -300,7 +363,8 @@ class _DecodeGraph:
   def _step(self):
     nxt, _, _ = self.model.next_token(self.cur[:, None], self.pos[:, None],
                                       self.cache, False, inplace=True)
-    ops.ops.decode_advance_(nxt, self.buf, self.step, self.pos, self.cur)
+    ops.ops.decode_advance_(nxt, self.buf, self.step, self.pos, self.cur,
+                            self.done, *self.eos_pad)
 
   @staticmethod
   def _copy_cache(dst_cache, src_cache, slots):
@@ -316,16 +380,25 @@ class _DecodeGraph:
         else:
           d.copy_(s_)
 
-  def run(self, cache, cur, pos, buf, step, n_more, all_done=None, events=None,
-          start=1, cache_len=None):
+  def run(self, cache, cur, pos, buf, step, n_more, events=None, start=1,
+          cache_len=None, done_in=None):
     """Replays the step `n_more` times from buffer column `start` (the
-    tokens before it are already in `buf`).  `cache_len`: tokens already in
-    the attention caches (host-known), so only written ring slots move."""
+    tokens before it are already in `buf`, the rest of `buf` is pad).
+    `cache_len`: tokens already in the attention caches (host-known), so
+    only written ring slots move.  Returns the per-row done flags."""
     dev_stream = torch.cuda.current_stream(cur.device)
+    steps = buf.shape[1]
     self._copy_cache(self.cache, cache, cache_len)
     self.cur.copy_(cur)
     self.pos.copy_(pos)
     self.step.fill_(start)
+    self.buf[:, :steps].copy_(buf)        # no columns left from an earlier run
+    if self.done is not None:
+      if done_in is not None:
+        self.done.copy_(done_in)
+      else:
+        self.done.zero_()
+    watch = _DoneWatch(self.done)
     self.stream.wait_stream(dev_stream)
     with torch.cuda.stream(self.stream):
       if events is not None:   # the replays alone (cache copies excluded)
@@ -335,18 +408,17 @@ class _DecodeGraph:
         events["decode_start"].record()
       done = 0
       for i in range(n_more):
+        if watch.finished(i):
+          break
         self.graph.replay()
         done += 1
-        if all_done is not None and (i % 8 == 7) and all_done(
-            self.buf[:, :buf.shape[1]]):
-          break
       if events is not None:
         events["decode_end"].record()
     dev_stream.wait_stream(self.stream)
-    steps = buf.shape[1]
     buf[:, start:].copy_(self.buf[:, start:steps])
     step.copy_(self.step)
     pos.copy_(self.pos)
     cur.copy_(self.cur)
     self._copy_cache(cache, self.cache,
                      None if cache_len is None else cache_len + done)
+    return _row_done(self.done, cur.shape[0], cur.device).clone()

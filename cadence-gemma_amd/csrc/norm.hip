@@ -253,22 +253,36 @@ __global__ __launch_bounds__(256) void segment_info_kernel(
 }
 
 // Greedy-decode bookkeeping on device (no host sync per step):
-// out[b, *step] = next[b]; pos[b] += 1; (++*step once).
+// out[b, *step] = next[b] (pad once row b has emitted EOS); pos[b] += 1;
+// cur[b] = the token written; done[b] latches on EOS, done[B] = all rows done
+// (read by the host a few steps late, so it never stalls the GPU); ++*step.
 __global__ void decode_advance_kernel(const int32_t* __restrict__ next,
                                       int32_t* __restrict__ out, int64_t ldo,
                                       int32_t* __restrict__ step,
                                       int32_t* __restrict__ pos,
-                                      int32_t* __restrict__ cur, int B) {
-  const int b = blockIdx.x * 256 + threadIdx.x;
+                                      int32_t* __restrict__ cur,
+                                      int32_t* __restrict__ done, int eos_id,
+                                      int pad_id, int B) {
+  const int b = threadIdx.x;
   const int s = *step;
+  int fin = 1;
   if (b < B) {
-    const int32_t t = next[b];
+    int32_t t = next[b];
+    if (done) {
+      const int d = done[b];
+      if (d) t = pad_id;
+      fin = d | (t == eos_id);
+      done[b] = fin;
+    }
     out[(int64_t)b * ldo + s] = t;
     pos[b] += 1;
     if (cur) cur[b] = t;
   }
-  __syncthreads();
-  if (blockIdx.x == 0 && threadIdx.x == 0) *step = s + 1;
+  const int all = __syncthreads_and(fin);
+  if (threadIdx.x == 0) {
+    *step = s + 1;
+    if (done) done[B] = all;
+  }
 }
 
 }  // namespace
@@ -277,12 +291,15 @@ extern "C" {
 
 int cadence_decode_advance(const int32_t* next_token, int32_t* tokens_out,
                            int64_t ld_out, int32_t* step, int32_t* positions,
-                           int32_t* cur_out, int64_t B, void* stream) {
+                           int32_t* cur_out, int32_t* done, int32_t eos_id,
+                           int32_t pad_id, int64_t B, void* stream) {
   if (B <= 0) return 0;
-  if (B > 256) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(256), 0,
+  if (B > 1024) return (int)hipErrorInvalidValue;
+  const unsigned threads = (unsigned)((B + 63) / 64 * 64);
+  hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(threads), 0,
                      static_cast<hipStream_t>(stream), next_token, tokens_out,
-                     ld_out, step, positions, cur_out, (int)B);
+                     ld_out, step, positions, cur_out, done, eos_id, pad_id,
+                     (int)B);
   return (int)hipGetLastError();
 }
 

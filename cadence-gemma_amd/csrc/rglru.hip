@@ -305,185 +305,189 @@ __global__ __launch_bounds__(64) void rnn_scan_kernel(ScanArgs p) {
   }
 }
 
-// ---------------------------------------------- LDS-staged scan (prefill)
+// ------------------------------------------- chunked (segmented) scan
 //
-// One wave per (sequence, 64-channel group); lane = channel.  Time is cut
-// into chunks of S steps; x / a / gate rows of a chunk (S x 128 B each) and
-// its positions move HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: one
-// instruction = 8 rows = 1 KiB), NB chunks in flight in an LDS ring.  That
-// is what lifts the bytes in flight: a register-staged scan is capped at 63
-// outstanding vector ops of 128-256 B per wave (~10 MB chip-wide), the DMA
-// ops carry 1 KiB each.  The recurrence itself is the exact sequential fp32
-// chain of layers.py:195-197; y rows are staged in LDS and leave as 16-B
-// stores.  vmcnt is managed by hand: loads and stores retire in order, so
-// "chunk c has landed" = at most (ops issued after it) outstanding.
-// Measured against the register engine once that one filled the chip with
-// one-wave workgroups, this variant is slower (4.4 vs 4.7 TB/s at NB=4; a
-// deeper ring costs residency), so it is an A/B option, not the default.
+// For batches too small to fill the chip with one lane per (sequence,
+// channel pair) -- B * E / 2 lanes is 1280 at B = 1, E = 2560 -- time is cut
+// into C chunks of S steps and every (sequence, 128-channel group, chunk)
+// gets its own wave.  A wave loads its chunk's x / a / gate / reset rows
+// into registers (all loads issued up front), then
+//   1. scans the chunk from h = 0, giving the chunk's affine summary
+//      h_end = P * h_in + H with P = prod(a * ~reset) (chunk 0 scans from h0
+//      exactly and publishes P = 0, H = its exact end state);
+//   2. publishes (P, H) per channel;
+//   3. carries h_in = P_j * h_in + H_j over the summaries of chunks
+//      j = 0 .. c-1 in that fixed order (deterministic: it never depends
+//      on which chunks finished first);
+//   4. rescans its register-resident chunk from h_in with the reference op
+//      order (layers.py:195-197) and writes y (and h_last from the last
+//      chunk).
+// HBM traffic stays one read of the inputs and one write of y; the summary
+// reads are L2 / MALL hits.  Chunks 0 and 1 are bit-exact with the
+// sequential chain; later chunks differ only through the carry's rounding
+// (the composed summaries round differently), which decays as a < 1.
+//
+// Publication needs no fence: the summary buffer starts as all-ones bits (a
+// NaN) and every summary float is written and read with agent-scope atomic
+// accesses (coherent across the XCDs' L2s); a reader spins per value until
+// it is not NaN.  (A release / acquire fence per wave -- an L2 write-back
+// plus invalidate -- cost ~40 us over 1600 waves.)  The waves of one
+// (sequence, channel group) take their chunk index from a counter of that
+// group in dispatch order, and chunk c only waits on chunks < c, so every
+// wait is on a wave that is already running; the wait is also bounded so a
+// fault cannot hang the GPU.
 
-typedef const void __attribute__((address_space(1)))* scan_gptr_t;
-typedef void __attribute__((address_space(3)))* scan_lptr_t;
+struct ChunkArgs {
+  float* agg;           // [B][C][4][E/2]: (P0, H0, P1, H1) planes per chunk
+  int32_t* ticket;      // [B][E/128] chunk counters, start at -1
+  int C;
+};
 
-template <int N>
-CADENCE_DEV void wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0xf70);
-  __asm__ volatile("" ::: "memory");
+CADENCE_DEV float bflo(uint32_t v) { return __uint_as_float(v << 16); }
+CADENCE_DEV float bfhi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
+
+CADENCE_DEV void agg_put(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+CADENCE_DEV float agg_get(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// wait for "BASE + k * NST ops still outstanding", k = 0..KMAX (runtime k)
-template <int BASE, int NST, int K, int KMAX>
-CADENCE_DEV void wait_sel(int k) {
-  if constexpr (K == KMAX) {
-    wait_vm<BASE + K * NST>();
-  } else {
-    if (k == K) wait_vm<BASE + K * NST>();
-    else wait_sel<BASE, NST, K + 1, KMAX>(k);
-  }
-}
-
-template <int S, int NB, bool GATE, bool POS>
-__global__ __launch_bounds__(64) void rnn_scan_lds_kernel(ScanArgs p) {
-  constexpr int RB = S * 64;                  // u16 per S x 64-channel slab
-  constexpr int NARR = 2 + (GATE ? 1 : 0);    // x, a, [gate]
-  constexpr int SLOT = NARR * RB + 128;       // u16 per ring slot (+ 64 pos)
-  constexpr int NLD = NARR * (S / 8) + (POS ? 1 : 0);
-  constexpr int NST = S / 8;
-  static_assert(S == 16, "ring-read offsets below assume 16-step chunks");
-  __shared__ __attribute__((aligned(16))) u16 lds[NB * SLOT];
-  __shared__ __attribute__((aligned(16))) u16 ylds[RB];   // never a DMA target
-
-  const int groups = p.E / 64;
-  const int b = blockIdx.x / groups;
-  const int e0 = (blockIdx.x % groups) * 64;
-  const int lane = threadIdx.x;
+template <int S, bool GATE, bool POS>
+__global__ __launch_bounds__(64) void rnn_scan_chunk_kernel(ScanArgs p,
+                                                            ChunkArgs c) {
+  const int G = p.E / 128;
+  const int BG = p.B * G;
+  const int bg = blockIdx.x % BG;
+  __shared__ int tk;
+  if (threadIdx.x == 0) tk = atomicAdd(c.ticket + bg, 1) + 1;
+  __syncthreads();
+  const int chunk = tk;
+  const int b = bg / G;
+  const int e = (bg - b * G) * 128 + threadIdx.x * 2;
+  const int lp = e >> 1;
+  const int t0 = chunk * S;
+  const int n = min(S, p.L - t0);
   const int64_t row0 = (int64_t)b * p.L;
-  const int nch = (p.L + S - 1) / S;
-
-  // per-lane DMA sources: row (lane / 8) of an 8-row piece, 16-B chunk lane % 8
-  const int prow = lane >> 3, pcol = (lane & 7) * 8;
-  auto issue = [&](int c) {
-    u16* slot = lds + (c % NB) * SLOT;
+  uint32_t xs[S], as[S], gs[S];
+  int32_t ps[S];
 #pragma unroll
-    for (int i = 0; i < S / 8; ++i) {
-      const int64_t t = min(c * S + i * 8 + prow, p.L - 1);   // clamp tail
-      __builtin_amdgcn_global_load_lds(
-          (scan_gptr_t)(p.x + (row0 + t) * p.ldx + e0 + pcol),
-          (scan_lptr_t)(slot + i * 512), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(
-          (scan_gptr_t)(p.a + (row0 + t) * p.lda + e0 + pcol),
-          (scan_lptr_t)(slot + RB + i * 512), 16, 0, 0);
-      if constexpr (GATE)
-        __builtin_amdgcn_global_load_lds(
-            (scan_gptr_t)(p.gate + (row0 + t) * p.ldg + e0 + pcol),
-            (scan_lptr_t)(slot + 2 * RB + i * 512), 16, 0, 0);
-    }
-    if constexpr (POS) {
-      const int64_t t = min(c * S + lane, p.L - 1);
-      __builtin_amdgcn_global_load_lds((scan_gptr_t)(p.pos + row0 + t),
-                                       (scan_lptr_t)(slot + NARR * RB), 4, 0, 0);
-    }
-  };
-
-  // h0 rides the DMA queue ahead of chunk 0 (a register load here would make
-  // the compiler drain the whole prologue before the loop).
-  __shared__ float hlds[64];
-  if (p.h0)
-    __builtin_amdgcn_global_load_lds((scan_gptr_t)(p.h0 + (int64_t)b * p.E + e0 + lane),
-                                     (scan_lptr_t)hlds, 4, 0, 0);
-  float h = 0.0f;
+  for (int i = 0; i < S; ++i) {           // clamped rows: branch-free loads
+    const int64_t t = row0 + t0 + min(i, n - 1);
+    xs[i] = *reinterpret_cast<const uint32_t*>(p.x + t * p.ldx + e);
+    as[i] = *reinterpret_cast<const uint32_t*>(p.a + t * p.lda + e);
+    if constexpr (GATE) gs[i] = *reinterpret_cast<const uint32_t*>(p.gate + t * p.ldg + e);
+    if constexpr (POS) ps[i] = p.pos[t];
+  }
+  float h0v = 0.f, h1v = 0.f;
+  if (chunk == 0 && p.h0) {
+    h0v = p.h0[(int64_t)b * p.E + e];
+    h1v = p.h0[(int64_t)b * p.E + e + 1];
+  }
+  // component u of chunk j for this lane: agg[(j * 4 + u) * E/2] (lanes of
+  // one wave are contiguous: every access instruction is 256 coalesced bytes)
+  const int64_t plane = p.E / 2;
+  float* agg = c.agg + (int64_t)b * c.C * 4 * plane + lp;
+  if (chunk != c.C - 1) {
+    // 1. summary of this chunk (from h0 for chunk 0, from 0 otherwise)
+    float P0 = 1.f, P1 = 1.f, H0 = h0v, H1 = h1v;
 #pragma unroll
-  for (int c = 0; c < NB - 1; ++c)
-    if (c < nch) issue(c);
-  for (int c = 0; c < nch; ++c) {
-    const bool more = c + NB - 1 < nch;
-    if (more) issue(c + NB - 1);
-    // chunk c landed: ops issued after it = NB-1 load groups + the store
-    // groups of the last min(c, NB-1) chunks; once the ring drains, wait all.
-    if (more) wait_sel<(NB - 1) * NLD, NST, 0, NB - 1>(min(c, NB - 1));
-    else wait_vm<0>();
-    // Ring reads go through inline asm: the compiler cannot tell ring slots
-    // apart and would otherwise put vmcnt(0) before every ds_read.
-    const uint32_t sbase =
-        (uint32_t)(uintptr_t)(scan_lptr_t)(lds + (c % NB) * SLOT);
-    const int steps = min(S, p.L - c * S);
-    if (c == 0 && p.h0) {
-      const uint32_t ha = (uint32_t)(uintptr_t)(scan_lptr_t)hlds + lane * 4;
-      asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)"
-                   : "=&v"(h) : "v"(ha) : "memory");
-    }
-    for (int i0 = 0; i0 < steps; i0 += 4) {
-      uint32_t xv[4], av[4], gv[4] = {0, 0, 0, 0};
-      int32_t pv[4] = {1, 1, 1, 1};
-      const uint32_t va = sbase + i0 * 128 + lane * 2;
-      asm volatile(
-          "ds_read_u16 %0, %8 offset:0\n"
-          "ds_read_u16 %1, %8 offset:128\n"
-          "ds_read_u16 %2, %8 offset:256\n"
-          "ds_read_u16 %3, %8 offset:384\n"
-          "ds_read_u16 %4, %8 offset:2048\n"
-          "ds_read_u16 %5, %8 offset:2176\n"
-          "ds_read_u16 %6, %8 offset:2304\n"
-          "ds_read_u16 %7, %8 offset:2432\n"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(xv[0]), "=&v"(xv[1]), "=&v"(xv[2]), "=&v"(xv[3]),
-            "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3])
-          : "v"(va) : "memory");
-      if constexpr (GATE)
-        asm volatile(
-            "ds_read_u16 %0, %4 offset:4096\n"
-            "ds_read_u16 %1, %4 offset:4224\n"
-            "ds_read_u16 %2, %4 offset:4352\n"
-            "ds_read_u16 %3, %4 offset:4480\n"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(gv[0]), "=&v"(gv[1]), "=&v"(gv[2]), "=&v"(gv[3])
-            : "v"(va) : "memory");
-      if constexpr (POS) {
-        const uint32_t pa = sbase + NARR * RB * 2 + i0 * 4;
-        asm volatile("ds_read_b128 %0, %1\n s_waitcnt lgkmcnt(0)"
-                     : "=&v"(*reinterpret_cast<int4*>(pv)) : "v"(pa) : "memory");
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (i0 + j < steps) {
-          float a = __uint_as_float(av[j] << 16);
-          if constexpr (POS) a = pv[j] == 0 ? 0.0f : a;   // a *= ~reset
-          h = add_rn(mul_rn(a, h), __uint_as_float(xv[j] << 16));
-          float y = rbf(h);
-          if constexpr (GATE) y = bmul(y, __uint_as_float(gv[j] << 16));
-          ylds[(i0 + j) * 64 + lane] = f2bf(y);
-        }
+    for (int i = 0; i < S; ++i) {
+      if (i < n) {
+        const bool r = POS && ps[i] == 0;
+        const float a0 = r ? 0.f : bflo(as[i]), a1 = r ? 0.f : bfhi(as[i]);
+        H0 = add_rn(mul_rn(a0, H0), bflo(xs[i]));
+        H1 = add_rn(mul_rn(a1, H1), bfhi(xs[i]));
+        P0 = mul_rn(P0, a0);
+        P1 = mul_rn(P1, a1);
       }
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): y slab written
-    __builtin_amdgcn_wave_barrier();
+    if (chunk == 0) P0 = P1 = 0.f;
+    // 2. publish
+    float* q = agg + (int64_t)chunk * 4 * plane;
+    agg_put(q, P0);
+    agg_put(q + plane, H0);
+    agg_put(q + 2 * plane, P1);
+    agg_put(q + 3 * plane, H1);
+  }
+  // 3. carry-in from the summaries of chunks 0 .. chunk-1, in order, 8 in
+  // flight; a value still NaN (not yet written) is polled again
+  for (int j0 = 0; j0 < chunk; j0 += 8) {
+    float v[8][4];
+    int spins = 0;
+    for (;;) {
+      bool ready = true;
 #pragma unroll
-    for (int i = 0; i < S / 8; ++i) {
-      const int r = i * 8 + prow;
-      const uint4 v = *reinterpret_cast<const uint4*>(ylds + r * 64 + pcol);
-      if (r < steps)
-        *reinterpret_cast<uint4*>(p.out + (row0 + c * S + r) * p.ldo + e0 + pcol) = v;
+      for (int k = 0; k < 8; ++k) {
+        const float* q = agg + (int64_t)min(j0 + k, chunk - 1) * 4 * plane;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[k][u] = agg_get(q + u * plane);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ready = ready && !__builtin_isnan(v[k][u]);
+      if (__all(ready) || ++spins > (1 << 20)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (j0 + k < chunk) {
+        h0v = add_rn(mul_rn(v[k][0], h0v), v[k][1]);
+        h1v = add_rn(mul_rn(v[k][2], h1v), v[k][3]);
+      }
     }
   }
-  if (p.h_last) p.h_last[(int64_t)b * p.E + e0 + lane] = h;
-  wait_vm<0>();   // no DMA may land after the workgroup's LDS is released
+  // 4. exact rescan from the carry-in, writing y
+  u16* op = p.out + (row0 + t0) * p.ldo + e;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    if (i < n) {
+      const bool r = POS && ps[i] == 0;
+      const float a0 = r ? 0.f : bflo(as[i]), a1 = r ? 0.f : bfhi(as[i]);
+      h0v = add_rn(mul_rn(a0, h0v), bflo(xs[i]));
+      h1v = add_rn(mul_rn(a1, h1v), bfhi(xs[i]));
+      float y0 = rbf(h0v), y1 = rbf(h1v);
+      if constexpr (GATE) {
+        y0 = bmul(y0, bflo(gs[i]));
+        y1 = bmul(y1, bfhi(gs[i]));
+      }
+      *reinterpret_cast<uint32_t*>(op + (int64_t)i * p.ldo) =
+          (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
+    }
+  }
+  if (chunk == c.C - 1 && p.h_last) {
+    p.h_last[(int64_t)b * p.E + e] = h0v;
+    p.h_last[(int64_t)b * p.E + e + 1] = h1v;
+  }
 }
 
-template <int S, int NB>
-bool launch_scan_lds(const ScanArgs& p, hipStream_t st) {
+// Chunk plan: 0 = the one-lane-per-sequence kernel (enough lanes to fill the
+// chip, or too short a sequence to cut), else the chunk length S: the
+// shortest of 8 / 16 / 32 / 64 steps that cuts L into at most 32 chunks
+// (64 for L up to 4096).
+int chunk_plan(int64_t B, int64_t L, int64_t E, int* chunks) {
+  const int64_t lanes = B * E / 2;
+  if (E % 128 || lanes >= 32768 || L < 16 || L > 4096) return 0;
+  int S = 8;
+  while (S < 64 && (L + S - 1) / S > 32) S *= 2;
+  *chunks = (int)((L + S - 1) / S);
+  return S;
+}
+
+int64_t chunk_ws_bytes(int64_t B, int64_t E, int64_t C) {
+  return B * (E / 2) * C * 16 + B * (E / 128) * 4 + 256;
+}
+
+template <int S>
+void launch_scan_chunked(const ScanArgs& p, const ChunkArgs& c, hipStream_t st) {
+  const dim3 grid((unsigned)((int64_t)p.B * (p.E / 128) * c.C)), block(64);
   const bool g = p.gate != nullptr, q = p.pos != nullptr;
-  auto al = [](const void* ptr, int64_t ld) {
-    return ((uintptr_t)ptr % 16 == 0) && ld % 8 == 0;
-  };
-  if (p.E % 64 || p.L < 2 * S || !al(p.x, p.ldx) || !al(p.a, p.lda) ||
-      !al(p.out, p.ldo) || (g && !al(p.gate, p.ldg)))
-    return false;
-  const dim3 grid((unsigned)((int64_t)p.B * (p.E / 64))), block(64);
-  if (g && q) hipLaunchKernelGGL((rnn_scan_lds_kernel<S, NB, true, true>), grid, block, 0, st, p);
-  else if (g) hipLaunchKernelGGL((rnn_scan_lds_kernel<S, NB, true, false>), grid, block, 0, st, p);
-  else if (q) hipLaunchKernelGGL((rnn_scan_lds_kernel<S, NB, false, true>), grid, block, 0, st, p);
-  else hipLaunchKernelGGL((rnn_scan_lds_kernel<S, NB, false, false>), grid, block, 0, st, p);
-  return true;
+  if (g && q) hipLaunchKernelGGL((rnn_scan_chunk_kernel<S, true, true>), grid, block, 0, st, p, c);
+  else if (g) hipLaunchKernelGGL((rnn_scan_chunk_kernel<S, true, false>), grid, block, 0, st, p, c);
+  else if (q) hipLaunchKernelGGL((rnn_scan_chunk_kernel<S, false, true>), grid, block, 0, st, p, c);
+  else hipLaunchKernelGGL((rnn_scan_chunk_kernel<S, false, false>), grid, block, 0, st, p, c);
 }
 
 template <int CPL, int CH>
@@ -550,40 +554,45 @@ int cadence_conv1d(const void* x, int64_t ldx, const void* w, const void* b,
   return (int)hipGetLastError();
 }
 
+int64_t cadence_rnn_scan_workspace_bytes(int64_t B, int64_t L, int64_t E) {
+  int C = 0;
+  if (!chunk_plan(B, L, E, &C)) return 0;
+  return chunk_ws_bytes(B, E, C);
+}
+
 int cadence_rnn_scan(const void* x, int64_t ldx, const void* a, int64_t lda,
                      const int32_t* segment_pos, const float* h0,
                      const void* gate, int64_t ldg, void* out, int64_t ldo,
                      float* h_last, int64_t B, int64_t L, int64_t E,
-                     void* stream) {
+                     void* workspace, int64_t ws_bytes, void* stream) {
   if (E % 2 || ldx % 2 || lda % 2 || ldo % 2 || (gate && ldg % 2))
     return (int)hipErrorInvalidValue;
   if (L <= 0 || B <= 0) return 0;
   ScanArgs p{static_cast<const u16*>(x), ldx, static_cast<const u16*>(a), lda,
              segment_pos, h0, static_cast<const u16*>(gate), ldg,
              static_cast<u16*>(out), ldo, h_last, (int)B, (int)L, (int)E};
-  // Default: two channels per lane, 16-step register ring, one-wave
-  // workgroups (4.7 TB/s at B=32, L=319/2048, E=2560 on MI355X).
-  // CADENCE_SCAN=reg1|lds4|lds6|lds8|reg2c8|reg2c12 selects the A/B variants
-  // (tools/scan_micro.py; the LDS-DMA ring measured 4.4 TB/s at NB=4 and
-  // loses residency beyond it).
   hipStream_t st = static_cast<hipStream_t>(stream);
-  static const int mode = [] {
-    const char* v = getenv("CADENCE_SCAN");
-    if (!v) return 0;
-    const char* names[] = {"reg2", "reg1", "lds4", "lds6", "lds8", "reg2c8", "reg2c12"};
-    for (int i = 0; i < 7; ++i)
-      if (!strcmp(v, names[i])) return i;
-    return 0;
-  }();
-  switch (mode) {
-    case 1: launch_scan<1, 16>(p, st); break;
-    case 2: if (!launch_scan_lds<16, 4>(p, st)) launch_scan<2, 16>(p, st); break;
-    case 3: if (!launch_scan_lds<16, 6>(p, st)) launch_scan<2, 16>(p, st); break;
-    case 4: if (!launch_scan_lds<16, 8>(p, st)) launch_scan<2, 16>(p, st); break;
-    case 5: launch_scan<2, 8>(p, st); break;
-    case 6: launch_scan<2, 12>(p, st); break;
-    default: launch_scan<2, 16>(p, st);
+  int C = 0;
+  const int S = chunk_plan(B, L, E, &C);
+  if (S && workspace && ws_bytes >= chunk_ws_bytes(B, E, C) &&
+      (uintptr_t)workspace % 16 == 0) {
+    // small batch: chunked scan (one wave per sequence x 128 channels x
+    // chunk); summaries start as NaN, chunk counters as -1 (one memset)
+    char* w = static_cast<char*>(workspace);
+    const int64_t agg_bytes = B * (E / 2) * C * 16;
+    ChunkArgs c{reinterpret_cast<float*>(w),
+                reinterpret_cast<int32_t*>(w + agg_bytes), C};
+    hipError_t e = hipMemsetAsync(w, 0xff, agg_bytes + B * (E / 128) * 4, st);
+    if (e != hipSuccess) return (int)e;
+    if (S == 8) launch_scan_chunked<8>(p, c, st);
+    else if (S == 16) launch_scan_chunked<16>(p, c, st);
+    else if (S == 32) launch_scan_chunked<32>(p, c, st);
+    else launch_scan_chunked<64>(p, c, st);
+    return (int)hipGetLastError();
   }
+  // Otherwise two channels per lane, 16-step register ring, one-wave
+  // workgroups (4.7 TB/s at B=32, L=319/2048, E=2560 on MI355X).
+  launch_scan<2, 16>(p, st);
   return (int)hipGetLastError();
 }
 

@@ -238,7 +238,16 @@ int cadence_rnn_scan(const void* x, int64_t ldx, const void* a, int64_t lda,
                      const int32_t* segment_pos, const float* h0,
                      const void* gate, int64_t ldg, void* out, int64_t ldo,
                      float* h_last, int64_t B, int64_t L, int64_t E,
-                     void* stream);
+                     void* workspace, int64_t ws_bytes, void* stream);
+
+/* Workspace bytes the chunked (segmented) form of cadence_rnn_scan needs
+ * for (B, L, E); 0 when the one-lane-per-sequence kernel is used.  With a
+ * workspace of at least this size, batches whose B * E / 2 lanes cannot
+ * fill the chip run time-chunked: per-chunk affine summaries, an in-order
+ * carry over them, and an exact rescan of each chunk from its carry-in
+ * (chunks 0 and 1 bit-exact; later chunks differ only through the carry's
+ * rounding).  workspace may be NULL: the sequential kernel then runs. */
+int64_t cadence_rnn_scan_workspace_bytes(int64_t B, int64_t L, int64_t E);
 
 /* ---- local attention ------------------------------------------------------ */
 
@@ -364,12 +373,16 @@ int cadence_splice_positions(const int32_t* text_pos, int32_t* out,
                              void* stream);
 
 /* Greedy decode bookkeeping (the host loop of examples/cadence_sampler.py:
- * 131-151 moved on device): tokens_out[b, *step] = next_token[b];
- * positions[b] += 1; *step += 1; cur_out[b] = next_token[b] (the next
- * step's input token; cur_out may be null).  B <= 256. */
+ * 131-151 and the done test of recurrentgemma/torch/sampler.py:217-223
+ * moved on device): tokens_out[b, *step] = next_token[b], or pad_id once
+ * row b has emitted eos_id; positions[b] += 1; *step += 1; cur_out[b] = the
+ * token written (the next step's input; cur_out may be null).  done (may be
+ * null: no EOS handling) is int32[B + 1]: done[b] latches when row b emits
+ * eos_id, done[B] = 1 when every row is done.  B <= 1024. */
 int cadence_decode_advance(const int32_t* next_token, int32_t* tokens_out,
                            int64_t ld_out, int32_t* step, int32_t* positions,
-                           int32_t* cur_out, int64_t B, void* stream);
+                           int32_t* cur_out, int32_t* done, int32_t eos_id,
+                           int32_t pad_id, int64_t B, void* stream);
 
 #ifdef __cplusplus
 }  // extern "C"

@@ -57,6 +57,69 @@ def test_shard_and_gather_gloo(world):
     assert t == world - 1 + 0.5
 
 
+def _bench_worker(rank, world, port, q):
+  """bench.py's own sharding (shard_plan), input generation (make_inputs)
+  and gather, with the CPU oracle's greedy sampler standing in for the GPU
+  step on a tiny multimodal model: each rank runs its micro-batches."""
+  os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+  import bench
+  r, w, _ = D.init_from_env(backend="gloo")
+  out = _bench_rows(r, w, bench)
+  D.barrier()
+  q.put((r, out.tolist()))
+  D.shutdown()
+
+
+def _bench_rows(rank, world, bench):
+  from oracle import griffin_ref as R
+  import test_model_gpu as M
+  gb, micro, size, prompt, steps = 8, 2, 28, 6, 3
+  cfg = M.small_config(vocab=128)
+  vis = M.tiny_vision(size)
+  torch.manual_seed(0)
+  import cadence
+  m = cadence.Griffin(cfg, dtype=torch.bfloat16, vision=vis)
+  p = {k: v.detach() for k, v in m.state_dict().items()}
+  lo, hi, sl = bench.shard_plan(gb, micro, rank, world)
+  tok, img = bench.make_inputs(gb, lo, hi, size, prompt, cfg.vocab_size, False)
+  outs = [R.greedy_sample(p, cfg, tok[s].long(), steps, pixels=img[s],
+                          vcfg=vis)[0].to(torch.int32) for s in sl]
+  return D.gather_rows(torch.cat(outs))
+
+
+def test_bench_sharding_matches_single_rank():
+  """World 2 over gloo through bench.py's sharding gives exactly the rows a
+  single rank computes for the whole global batch (per-sample image seeds,
+  one token stream, contiguous blocks, one gather)."""
+  import bench
+  want = _bench_rows(0, 1, bench).tolist()
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q))
+           for r in range(2)]
+  for p in procs:
+    p.start()
+  res = [q.get(timeout=300) for _ in procs]
+  for p in procs:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  for _, out in res:
+    assert out == want
+
+
+def test_bench_shard_plan():
+  import bench
+  assert bench.shard_plan(256, 32, 0, 1)[2][-1] == slice(224, 256)
+  lo, hi, sl = bench.shard_plan(256, 32, 3, 8)
+  assert (lo, hi, len(sl)) == (96, 128, 1)
+  lo, hi, sl = bench.shard_plan(256, 32, 1, 2)
+  assert (lo, hi, len(sl)) == (128, 256, 4)
+  with pytest.raises(ValueError):
+    bench.shard_plan(256, 48, 0, 2)
+
+
 def test_shard_range_contract():
   assert D.shard_range(256, 3, 8) == (96, 128)
   with pytest.raises(ValueError):

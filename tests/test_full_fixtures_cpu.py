@@ -1,0 +1,88 @@
+"""CPU checks of the full-size fixtures (tests/golden/full_*.safetensors).
+
+The GPU test (test_full_size_gpu.py) rebuilds 3.4 G fixture weights on the
+device; here the hash generator itself is pinned (known values, exactness
+of the uniform grid) and every fixture is checked for shape / content
+consistency, with the probe values of its smaller tensors recomputed on
+the CPU (the full rebuild takes ~90 s per configuration on 8 cores, too
+slow for the CPU suite; make_golden_full.py does it when regenerating).
+"""
+
+import os
+import sys
+
+import pytest
+import torch
+from safetensors import safe_open
+from safetensors.torch import load_file
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import hashinit as H  # noqa: E402
+import make_golden_full as MG  # noqa: E402
+
+
+def test_hash_known_values_and_grid():
+  u = H.hash_uniform(6, 5, "cpu")
+  # exact multiples of 2^-24 in [0, 1)
+  assert torch.equal(u * 2 ** 24, torch.floor(u * 2 ** 24))
+  assert bool(((u >= 0) & (u < 1)).all())
+  # pinned: a change of the hash would silently invalidate every fixture
+  want = torch.tensor([H._lowbias32(torch.tensor([i ^ ((5 * 0x9E3779B1) & 0xFFFFFFFF)],
+                                                 dtype=torch.int64)).item() >> 8
+                       for i in range(6)], dtype=torch.float32) * 2.0 ** -24
+  assert torch.equal(u, want)
+  # lowbias32 reference values (Wellons' published constants, 32-bit math)
+  def ref(x):
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    return x ^ (x >> 16)
+  xs = [0, 1, 12345, 0xFFFFFFFF, 0x80000000]
+  got = H._lowbias32(torch.tensor(xs, dtype=torch.int64)).tolist()
+  assert got == [ref(x) for x in xs]
+  # statistics of a hashed tensor
+  t = H.hash_tensor((1 << 16,), 3, std=0.5, mean=1.0, dtype=torch.float32)
+  assert abs(float(t.mean()) - 1.0) < 0.01 and abs(float(t.std()) - 0.5) < 0.01
+
+
+@pytest.mark.parametrize("name", list(MG.CONFIGS))
+def test_full_fixture_consistent(name):
+  path = os.path.join(HERE, "golden", f"full_{name}.safetensors")
+  with safe_open(path, "pt") as f:
+    meta = f.metadata()
+  f = load_file(path)
+  size, b, t, steps, seed = MG.CONFIGS[name]
+  cfg, vis = MG.griffin_config(), MG.vision_config(size)
+  assert torch.equal(f["tokens"], MG.inputs(name)[0])
+  assert f["logit_idx"].shape[:2] == (b, 1 + steps)
+  assert f["logit_val"].shape == f["logit_idx"].shape
+  assert f["greedy_tokens"].shape == (b, steps)
+  assert int(f["logit_idx"].max()) < cfg.vocab_size
+  # the oracle's greedy tokens are the argmax of its stored step logits
+  for i in range(b):
+    for s in range(steps):
+      idx, val = f["logit_idx"][i, 1 + s], f["logit_val"][i, 1 + s]
+      assert int(idx[val.argmax()]) == int(f["greedy_tokens"][i, s])
+  if vis is not None:
+    assert f["features"].shape == (b, MG.N_FEATURE_ROWS, vis.feature_width)
+    assert f["image_tokens"].shape == (b, MG.N_FEATURE_ROWS, cfg.width)
+  shapes = MG.state_shapes(cfg, vis)
+  keys = sorted(shapes)
+  assert ",".join(keys) == meta["param_keys"]
+  probes = f["param_probes"]
+  for j, k in enumerate(keys):
+    n = 1
+    for d in shapes[k]:
+      n *= d
+    if n > (1 << 20):
+      continue
+    # hash_params seeds by the sorted position: rebuild with the same index
+    kind, std, mean = H.param_spec(k, tuple(shapes[k]), cfg.num_layers)
+    pseed = seed * 100003 + j
+    if kind == "a":
+      v = H._rnn_a_param(n, pseed).to(torch.bfloat16).view(*shapes[k])
+    else:
+      v = H.hash_tensor(tuple(shapes[k]), pseed, std, mean)
+    assert torch.equal(H.probes({k: v})[0], probes[j]), k

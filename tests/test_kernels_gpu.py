@@ -35,8 +35,35 @@ def two_doc_positions(b, t, split):
 
 # ------------------------------------------------------------------ scan
 
+def _chunked(b, t, e):
+  """True when cadence_rnn_scan takes the time-chunked form for this shape."""
+  from cadence import _lib
+  return _lib.load().cadence_rnn_scan_workspace_bytes(b, t, e) > 0
+
+
+def assert_scan(y, y_ref, h, h_ref, b, t, e):
+  """Bit-exact for the sequential kernel; for the chunked form (small
+  batches) the first two chunks (>= 16 steps) are bit-exact and later
+  chunks differ only through the carry's rounding: >= 99.5 % of y
+  bit-equal, within one bf16 ulp elsewhere, fp32 h_last to rtol 1e-4."""
+  y, h = y.cpu().view(y_ref.shape), h.cpu()
+  if not _chunked(b, t, e):
+    assert torch.equal(y, y_ref)
+    assert torch.equal(h, h_ref)
+    return
+  y, y_ref = y.view(b, t, e), y_ref.view(b, t, e)
+  assert torch.equal(y[:, :16], y_ref[:, :16])
+  frac = (y == y_ref).float().mean().item()
+  assert frac >= 0.995, frac
+  torch.testing.assert_close(y.float(), y_ref.float(), rtol=8e-3, atol=1e-5)
+  torch.testing.assert_close(h, h_ref, rtol=1e-4, atol=1e-5)
+
+
 @pytest.mark.parametrize("b,t,e,with_h0", [(2, 32, 128, True), (3, 129, 256, False),
-                                           (1, 1, 64, True), (4, 320, 2560, True)])
+                                           (1, 1, 64, True), (4, 320, 2560, True),
+                                           (1, 319, 2560, False),
+                                           (1, 2048, 2560, True),
+                                           (26, 64, 2560, True)])
 def test_rnn_scan_bitexact(dev, b, t, e, with_h0):
   g = torch.Generator().manual_seed(0)
   x = rnd(b, t, e, gen=g)
@@ -47,8 +74,27 @@ def test_rnn_scan_bitexact(dev, b, t, e, with_h0):
   y_ref, h_ref = R.rnn_scan(x, a, reset, h0)
   y, h = cadence.rnn_scan(x.to(dev), a.to(dev), reset.to(dev),
                           None if h0 is None else h0.to(dev))
-  assert torch.equal(y.cpu(), y_ref)
-  assert torch.equal(h.cpu(), h_ref)
+  assert_scan(y, y_ref, h, h_ref, b, t, e)
+
+
+def test_rnn_scan_chunked_long_decay(dev):
+  """Chunked scan with a close to 1 (slow decay: carry errors persist
+  longest) and no resets, B = 1, T = 2048: still within the chunk bar."""
+  g = torch.Generator().manual_seed(7)
+  b, t, e = 1, 2048, 1280
+  assert _chunked(b, t, e)
+  x = rnd(b, t, e, gen=g)
+  a = (0.999 - 0.01 * torch.rand(b, t, e, generator=g)).to(BF)
+  reset = torch.zeros(b, t, dtype=torch.bool)
+  y_ref, h_ref = R.rnn_scan(x, a, reset, None)
+  y, h = cadence.rnn_scan(x.to(dev), a.to(dev), reset.to(dev), None)
+  assert_scan(y, y_ref, h, h_ref, b, t, e)
+  # in place form (h0 and h_last alias) continues the same state
+  hh = torch.zeros(b, e, device=dev)
+  y2 = ops.ops.rnn_scan_(x.view(-1, e).to(dev), a.view(-1, e).to(dev), hh,
+                         None, b, t)
+  assert torch.equal(y2.view(b, t, e).cpu(), y.cpu())
+  assert torch.equal(hh.cpu(), h.cpu())
 
 
 @pytest.mark.parametrize("t,e,strided,with_h0", [(70, 512, False, False),
@@ -72,8 +118,7 @@ def test_rnn_scan_gated_matches_join(dev, t, e, strided, with_h0):
   got, h = ops.ops.rnn_scan(x.view(-1, e).to(dev), a.view(-1, e).to(dev),
                             pos.to(dev), None if h0 is None else h0.to(dev),
                             gate_d, b, t)
-  assert torch.equal(got.view(b, t, e).cpu(), want)
-  assert torch.equal(h.cpu(), h_ref)
+  assert_scan(got, want, h, h_ref, b, t, e)
 
 
 # ---------------------------------------------------------------- conv1d

@@ -1,0 +1,106 @@
+"""Sampler stopping and sampling modes on the GPU.
+
+EOS handling follows the intent of recurrentgemma/torch/sampler.py:177-223
+(`done |= next_token == eos`, loop while any row is not done) with per-row
+flags kept on the device by `decode_advance`: once a row emits EOS the rest
+of its buffer is pad, and the host stops issuing steps once every row is
+done (it reads the flag a few steps late; late steps only write pad).
+Categorical sampling (`greedy_sampling=False`, sampler.py:130-136).
+"""
+
+import pytest
+import torch
+
+import cadence
+from test_model_gpu import MockVocab, make_model, small_config
+
+pytestmark = pytest.mark.gpu
+
+
+class EosVocab(MockVocab):
+  def __init__(self, eos):
+    self._eos = eos
+
+  def eos_id(self):
+    return self._eos
+
+
+def _expected_with_eos(free, eos, pad):
+  want = free.clone()
+  for r in range(want.shape[0]):
+    hit = (want[r] == eos).nonzero()
+    if len(hit):
+      want[r, int(hit[0]) + 1:] = pad
+  return want
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_eos_stop_pads_rows_and_graph_reuse(dev, use_graph):
+  cfg = small_config(vocab=64, window=32)
+  m, _ = make_model(dev, cfg, seed=31)
+  b, steps = 4, 40
+  runs = []
+  for seed, t in ((1, 20), (2, 11)):
+    g = torch.Generator().manual_seed(seed)
+    tok = torch.randint(3, cfg.vocab_size, (b, t), generator=g, dtype=torch.int32)
+    runs.append((tok, torch.full((b,), t, dtype=torch.int32)))
+  free = [cadence.Sampler(m, MockVocab(), use_graph=False).generate(
+      tok, lens, steps).tokens_buffer.cpu() for tok, lens in runs]
+  # the most frequent generated token of the first run acts as EOS
+  eos = int(torch.mode(free[0].flatten()).values)
+  s = cadence.Sampler(m, EosVocab(eos), use_graph=use_graph)
+  for (tok, lens), fr in zip(runs, free):
+    # same sampler twice (graph and its static buffers reused), stop on EOS
+    st = s.generate(tok, lens, steps, end_sampling_at_eos_token=True)
+    want = _expected_with_eos(fr, eos, 0)
+    assert torch.equal(st.tokens_buffer.cpu(), want)
+    hit = (fr == eos).any(dim=1)
+    assert torch.equal(st.done.cpu(), hit)
+  # without EOS stopping the same sampler reproduces the free run
+  st = s.generate(*runs[0], steps, end_sampling_at_eos_token=False)
+  assert torch.equal(st.tokens_buffer.cpu(), free[0])
+
+
+def test_eos_all_rows_finish_early(dev):
+  """Every row emits EOS at its first token: the loop ends long before
+  `steps` and every later column is pad."""
+  cfg = small_config(vocab=64, window=32)
+  m, _ = make_model(dev, cfg, seed=32)
+  tok = torch.full((3, 6), 5, dtype=torch.int32)
+  lens = torch.full((3,), 6, dtype=torch.int32)
+  first = cadence.Sampler(m, MockVocab(), use_graph=False).generate(
+      tok, lens, 2).tokens_buffer.cpu()[:, 0]
+  assert bool((first == first[0]).all())       # identical rows
+  s = cadence.Sampler(m, EosVocab(int(first[0])), use_graph=True)
+  st = s.generate(tok, lens, 64, end_sampling_at_eos_token=True)
+  buf = st.tokens_buffer.cpu()
+  assert torch.equal(buf[:, 0], first)
+  assert bool((buf[:, 1:] == 0).all())
+  assert int(st.step) < 64                     # stopped early
+  assert bool(st.done.all())
+
+
+def test_categorical_sampling(dev):
+  """greedy_sampling=False: the first cached step and the loop both sample
+  from logits (the first step used to receive logits=None)."""
+  cfg = small_config(vocab=64, window=32)
+  m, _ = make_model(dev, cfg, seed=33)
+  with torch.no_grad():      # near-flat logits so samples differ from argmax
+    m.embedder.input_embedding.mul_(0.01)
+  g = torch.Generator().manual_seed(3)
+  tok = torch.randint(3, cfg.vocab_size, (2, 9), generator=g, dtype=torch.int32)
+  lens = torch.full((2,), 9, dtype=torch.int32)
+  s = cadence.Sampler(m, MockVocab(), greedy_sampling=False)
+  torch.manual_seed(123)
+  a = s.generate(tok, lens, 12).tokens_buffer.cpu()
+  torch.manual_seed(123)
+  b = s.generate(tok, lens, 12).tokens_buffer.cpu()
+  assert a.shape == (2, 12) and torch.equal(a, b)
+  assert bool(((a >= 0) & (a < cfg.vocab_size)).all())
+  torch.manual_seed(124)
+  c = s.generate(tok, lens, 12, return_logits=True)
+  assert c.logits_buffer.shape == (2, 12, 64)
+  greedy = cadence.Sampler(m, MockVocab()).generate(tok, lens, 12).tokens_buffer
+  assert not torch.equal(a, greedy.cpu())
+  out = s(["Hello ! How are you?"], 5)
+  assert out.tokens[0].shape == (5,)
