@@ -152,7 +152,7 @@ def _big_key(epi: str, M: int, N: int, K: int, groups: int = 1) -> str:
   """The rocprof name of the prefill GEMM kernel a launch runs:
   gemm_big_kernel<Epi, P8, MR> (tile height 32 MR, cadence_gemm_tile_rows)."""
   rows = _lib.load().cadence_gemm_tile_rows(M, N, K, groups)
-  p8 = 1 if (K % 128 == 0 and os.environ.get("CADENCE_GEMM_P8", "1") != "0") else 0
+  p8 = 1 if K % 128 == 0 else 0
   return f"gemm_big_kernel<{epi}, {p8}, {rows // 32}>"
 
 
@@ -181,7 +181,6 @@ def _ws(M: int, N: int, K: int, groups: int, like: torch.Tensor):
 
 # ------------------------------------------------------ packed decode rows
 
-DECODE_PACKED = os.environ.get("CADENCE_DECODE_PACKED", "1") != "0"
 
 
 class PackedRows(NamedTuple):
@@ -214,7 +213,7 @@ class PackedRows(NamedTuple):
 
 
 def want_packed(m: int, k: int) -> bool:
-  return DECODE_PACKED and 0 < m <= 32 and k % 32 == 0
+  return 0 < m <= 32 and k % 32 == 0
 
 
 def packed_empty(m: int, k: int, device) -> torch.Tensor:

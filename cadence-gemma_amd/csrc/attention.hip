@@ -732,13 +732,8 @@ int cadence_vit_attention(const void* qkv, void* out, int64_t B, int64_t N,
                           int64_t H, int64_t hd, void* stream) {
   if (hd != 64 && hd != 72) return (int)hipErrorInvalidValue;
   if (B <= 0 || N <= 0) return 0;
-  // LDS-resident swapped-QK^T kernel (vit_attention.hip) for short sequences;
-  // CADENCE_VIT_ATTN=flash keeps the streaming flash kernel (A/B runs).
-  static const bool flash_only = [] {
-    const char* e = getenv("CADENCE_VIT_ATTN");
-    return e && strncmp(e, "flash", 5) == 0;
-  }();
-  if (!flash_only) {
+  // LDS-resident swapped-QK^T kernel (vit_attention.hip) for short sequences
+  {
     const int rc = vit_attention_lds_launch(qkv, out, B, N, H, hd, stream);
     if (rc >= 0) return rc;
   }
@@ -797,13 +792,7 @@ int cadence_local_attention_decode(const void* q, const void* k_new,
                (int)window, 1.0f / sqrtf((float)hd),
                static_cast<float*>(workspace), sems};
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // window splits per sequence (CADENCE_DECODE_ATTN_SPLITS, 1..8, for A/B)
-  static const int nsplit = [] {
-    const char* e = getenv("CADENCE_DECODE_ATTN_SPLITS");
-    const int v = e ? atoi(e) : kDecodeSplits;
-    return v >= 1 && v <= kDecodeSplits ? v : kDecodeSplits;
-  }();
-  const dim3 grid((unsigned)B, split ? nsplit : 1);
+  const dim3 grid((unsigned)B, split ? kDecodeSplits : 1);
   if (hd == 256)
     hipLaunchKernelGGL(decode_attn_kernel<256>, grid, dim3(256), 0, st, a);
   else if (hd == 128)

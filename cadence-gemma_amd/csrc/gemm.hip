@@ -18,7 +18,6 @@
 //    into MFMA B fragments, split-K over the grid, fp32 partial slabs reduced
 //    in a fixed order (deterministic) by a second kernel that applies the
 //    same epilogue.
-//  * legacy 128x128 register-staged tile engine (CADENCE_GEMM_LEGACY=1).
 //
 // Epilogues replicate the reference rounding points:
 //  EpiLinear      nn.Linear (+bias) [+GELU(erf)] [+residual], row remap
@@ -59,7 +58,7 @@ CADENCE_DEV float softcap(float l, float c) {
 }
 
 // Epilogue interface.
-//  * Direct path (legacy tile, stream and split-K engines): apply(m, n, v, g)
+//  * Direct path (stream and split-K engines): apply(m, n, v, g)
 //    / apply2(m, f, v_gate, v_up, g) write one element.
 //  * Staged path (big engine, kStaged): bias_at() + stage() / stage2() take
 //    one accumulator to its first bf16 rounding point (bias added); the
@@ -489,135 +488,6 @@ struct EpiPatch {
 
 // Paired epilogues take the (gate, up) halves of each 64-column group:
 // packed column 64g + w (w < 32) pairs with 64g + 32 + w -> logical 32g + w.
-
-// ------------------------------------------------------------ tile engine
-
-template <int BM, int BN, class Epi>
-__global__ __launch_bounds__(256, 2) void gemm_tile_kernel(
-    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
-    int64_t ldw, int M, int N, int K, int64_t a_goff, int64_t w_goff,
-    Epi epi) {
-  constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
-  constexpr int ACH = BM * 8 / 256, BCH = BN * 8 / 256;  // 16-B chunks/thread
-  __shared__ uint4 smem[2][(BM + BN) * 8];
-
-  const int g = blockIdx.y;
-  A += g * a_goff;
-  W += g * w_goff;
-
-  const int ntm = (M + BM - 1) / BM, ntn = N / BN, nt = ntm * ntn;
-  int t = blockIdx.x;
-  {  // bijective XCD remap: blocks sharing an XCD get a contiguous tile range
-    const int xcd = t & 7, q = nt >> 3, r = nt & 7;
-    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-    t = base + (t >> 3);
-  }
-  constexpr int GM = 8;
-  const int grp = t / (GM * ntn), fm = grp * GM;
-  const int gs = min(ntm - fm, GM);
-  const int within = t % (GM * ntn);
-  const int tm = fm + within % gs, tn = within / gs;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int lrow = tid >> 3, lch = tid & 7;
-
-  uint4 ra[ACH], rb[BCH];
-  const uint4 zero = make_uint4(0, 0, 0, 0);
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      const int r = lrow + 32 * i;
-      const int gr = m0 + r;
-      ra[i] = gr < M ? ld16(A + (int64_t)gr * lda + k0 + lch * 8) : zero;
-    }
-#pragma unroll
-    for (int i = 0; i < BCH; ++i) {
-      const int r = lrow + 32 * i;
-      rb[i] = ld16(W + (int64_t)(n0 + r) * ldw + k0 + lch * 8);
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      const int r = lrow + 32 * i;
-      smem[buf][r * 8 + (lch ^ (r & 7))] = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BCH; ++i) {
-      const int r = lrow + 32 * i;
-      smem[buf][(BM + r) * 8 + (lch ^ (r & 7))] = rb[i];
-    }
-  };
-
-  f32x4 acc[MR][NR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[MR], bfr[NR];
-      const int ch = s * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < MR; ++i) {
-        const int r = wm * WM + i * 16 + (lane & 15);
-        af[i] = __builtin_bit_cast(bf16x8, smem[cur][r * 8 + (ch ^ (r & 7))]);
-      }
-#pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        const int r = wn * WN + j * 16 + (lane & 15);
-        bfr[j] = __builtin_bit_cast(bf16x8,
-                                    smem[cur][(BM + r) * 8 + (ch ^ (r & 7))]);
-      }
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-#pragma unroll
-        for (int j = 0; j < NR; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j],
-                                                              acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
-  }
-
-  // Epilogue: C/D layout of 16x16x32 -> col = lane & 15, row = 4*(lane>>4)+r.
-  const int mbase = m0 + wm * WM, nbase = n0 + wn * WN;
-  const int rsub = (lane >> 4) * 4, csub = lane & 15;
-  if constexpr (Epi::kPaired) {
-    static_assert(NR == 4, "paired epilogue needs 64-column wave tiles");
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mbase + i * 16 + rsub + r;
-          if (row < M)
-            epi.apply2(row, nbase / 2 + j * 16 + csub, acc[i][j][r],
-                       acc[i][j + 2][r], g);
-        }
-  } else {
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mbase + i * 16 + rsub + r;
-          if (row < M) epi.apply(row, nbase + j * 16 + csub, acc[i][j][r], g);
-        }
-  }
-}
 
 // ------------------------------------------------- big tile engine (DMA)
 //
@@ -1388,15 +1258,10 @@ __global__ __launch_bounds__(512) void reduce_rmsnorm_kernel(
   }
 }
 
-// Weight-streaming plan for M <= 32 (CADENCE_DECODE_ENGINE=splitk selects the
-// split-K skinny engine instead, for A/B runs): k-steps per wave (KSW) and K
-// splits so that one split is <= 8 * KSW steps.
+// Weight-streaming plan for M <= 32: k-steps per wave (KSW) and K splits so
+// that one split is <= 8 * KSW steps.
 int stream_plan(int64_t M, int64_t K, int* ksw, int* splits) {
-  static const bool off = [] {
-    const char* e = getenv("CADENCE_DECODE_ENGINE");
-    return e && strncmp(e, "splitk", 6) == 0;
-  }();
-  if (M > 32 || K % 32 || off) return 0;
+  if (M > 32 || K % 32) return 0;
   const int64_t ks = K / 32;
   if (ks <= 8) { *ksw = 1; *splits = 1; }
   else if (ks <= 16) { *ksw = 2; *splits = 1; }
@@ -1410,27 +1275,16 @@ int stream_plan(int64_t M, int64_t K, int* ksw, int* splits) {
 // K (the 2560-wide output projections) is split in two as well: 32
 // columns x one K half per workgroup halve the activation bytes each
 // workgroup pulls, and the reduce kernel replaces the norm launch (decode
-// step -50 us; CADENCE_OUTPROJ_SPLIT=1 keeps one split for A/B runs).
+// step -50 us).
 int rmsnorm_stream_plan(int64_t M, int64_t K, int* ksw, int* splits) {
-  static const bool split2 = [] {
-    const char* e = getenv("CADENCE_OUTPROJ_SPLIT");
-    return !(e && e[0] == '1');
-  }();
   if (!stream_plan(M, K, ksw, splits)) return 0;
   if (*splits >= 2 && *splits <= 4) return 1;
-  if (split2 && *splits == 1 && *ksw == 10 && K == 2560) {
+  if (*splits == 1 && *ksw == 10 && K == 2560) {
     *ksw = 5;
     *splits = 2;
     return 1;
   }
   return 0;
-}
-
-// CADENCE_GEMM_LEGACY=1 selects the 128x128 register-staged tile kernel
-// (A/B comparisons in one binary).
-bool use_legacy_tile() {
-  const char* e = getenv("CADENCE_GEMM_LEGACY");
-  return e && e[0] == '1';
 }
 
 int skinny_splits(int64_t N, int64_t K, int64_t groups) {
@@ -1489,22 +1343,13 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
 
 // Prefill engine plan for M > kSkinnyMaxM: 0 = 2-buffer 256-row kernel,
 // 256 / 224 = 8-phase kernel with that tile height.
-//  * 8-phase when K splits into pairs of 64-deep tiles (CADENCE_GEMM_P8=0
-//    keeps the 2-buffer schedule for A/B runs; an A/B of the guide's
-//    two-barrier phase -- reads, barrier, lgkmcnt(0), MFMAs, barrier -- ran
-//    1-5 % slower on every prefill shape);
+//  * 8-phase when K splits into pairs of 64-deep tiles (an A/B of the
+//    guide's two-barrier phase -- reads, barrier, lgkmcnt(0), MFMAs,
+//    barrier -- ran 1-5 % slower on every prefill shape);
 //  * tile height 256 or 224 rows, whichever needs fewer (rounds x rows) on
 //    the CUs (M = 10208 = 32 x 319: 460 tiles of 224 in 2 rounds beat 400 of
-//    256 in 2 rounds); CADENCE_GEMM_BM=256|224 forces one.
+//    256 in 2 rounds).
 int big_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
-  static const bool p8_off = [] {
-    const char* e = getenv("CADENCE_GEMM_P8");
-    return e && e[0] == '0';
-  }();
-  static const int bm_force = [] {
-    const char* e = getenv("CADENCE_GEMM_BM");
-    return e ? atoi(e) : 0;
-  }();
   static const int cus = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -1513,14 +1358,13 @@ int big_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
       n = 256;
     return n;
   }();
-  if (p8_off || K % (2 * BK) != 0) return 0;
+  if (K % (2 * BK) != 0) return 0;
   const int64_t ntn = (N + 255) / 256;
   auto rounds_x_rows = [&](int64_t bm) {
     const int64_t t = ((M + bm - 1) / bm) * ntn * groups;
     return ((t + cus - 1) / cus) * bm;
   };
-  if (bm_force == 224) return 224;
-  if (bm_force != 256 && rounds_x_rows(224) < rounds_x_rows(256)) return 224;
+  if (rounds_x_rows(224) < rounds_x_rows(256)) return 224;
   return 256;
 }
 
@@ -1536,14 +1380,6 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
   if (lda == 0 && (M > 32 || K % 32)) return (int)hipErrorInvalidValue;   // packed rows
   if (M > kSkinnyMaxM) {
     if (N % 64 || K % BK) return (int)hipErrorInvalidValue;
-    if (use_legacy_tile() && N % 128 == 0) {
-      const int64_t tiles = ((M + 127) / 128) * (N / 128);
-      dim3 grid((unsigned)tiles, (unsigned)groups);
-      hipLaunchKernelGGL((gemm_tile_kernel<128, 128, Epi>), grid, dim3(256), 0, st,
-                         A, lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff,
-                         epi);
-      return (int)hipGetLastError();
-    }
     const int rows = big_tile_rows(M, N, K, groups);
     const bool p8 = rows != 0;
     const bool bm224 = rows == 224;

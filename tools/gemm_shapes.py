@@ -1,6 +1,5 @@
 """Prefill GEMM sweep: ops.linear over (M, N, K) shapes, HIP-event time per
-launch and TFLOP/s / output GB/s.  CADENCE_GEMM_LEGACY=1 selects the 128x128
-engine (read once per process)."""
+launch and TFLOP/s / output GB/s."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cadence-gemma_amd"), ROOT]
@@ -33,7 +32,7 @@ def main():
                            "2048x5120x256,10208x5120x2560,10208x2560x2560,"
                            "10208x2560x7680,8352x1024x1024,8352x3072x1024,"
                            "8192x4352x1152").split(",")]
-  tag = "legacy" if os.environ.get("CADENCE_GEMM_LEGACY") == "1" else "big"
+  tag = "big"
   for M, N, K in shapes:
     a = torch.randn(M, K, device=dev).to(BF)
     w = (torch.randn(N, K, device=dev) / K ** .5).to(BF)

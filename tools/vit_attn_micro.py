@@ -1,6 +1,5 @@
 """ViT attention microbenchmark at the bench shapes (bs=32, 224 px): DINO
-(N=261, 16 heads x 64) and SigLIP (N=256, 16 x 72).  CADENCE_VIT_ATTN=flash
-selects the streaming flash kernel (read once per process).  Reports device
+(N=261, 16 heads x 64) and SigLIP (N=256, 16 x 72).  Reports device
 time per launch (graph-captured), MFMA TFLOP/s (4*B*H*N^2*hd) and HBM GB/s
 of the algorithmic bytes (qkv in + out)."""
 import os, sys
