@@ -55,7 +55,7 @@ _SIGS: dict[str, list] = {
     "cadence_gemm_logits": [P, I64, P, I64, I64, I64, I64, F32, P, I64, P, I64, P],
     "cadence_rmsnorm": [P, I64, P, P, I64, I64, I64, F32, P],
     "cadence_layernorm": [P, I64, P, P, P, I64, I64, I64, F32, P],
-    "cadence_embed": [P, P, P, I64, I64, I64, F32, I64, I64, I64, P],
+    "cadence_embed": [P, P, P, I64, I64, I64, I64, F32, I64, I64, I64, P],
     "cadence_conv1d": [P, I64, P, P, P, P, P, I64, P, I64, I64, I64, I64, I32,
                        P],
     "cadence_rnn_scan": [P, I64, P, I64, P, P, P, I64, P, I64, P, I64, I64, I64,

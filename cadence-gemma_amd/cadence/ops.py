@@ -127,14 +127,16 @@ class KernelTimer:
       return
     end = self._event()
     end.record(torch.cuda.current_stream(t.device))
-    self.records.setdefault(key + self.scope, []).append((ev, end, float(work)))
+    if not isinstance(work, torch.Tensor):
+      work = float(work)
+    self.records.setdefault(key + self.scope, []).append((ev, end, work))
 
   def summary(self) -> dict[str, dict]:
     torch.cuda.synchronize()
     out = {}
     for key, recs in self.records.items():
       ms = [a.elapsed_time(b) for a, b, _ in recs]
-      work = [w for _, _, w in recs]
+      work = [float(w) for _, _, w in recs]   # device scalars sync here
       out[key] = dict(launches=len(recs), total_ms=sum(ms),
                       avg_ms=sum(ms) / len(ms), avg_work=sum(work) / len(work),
                       total_work=sum(work))
@@ -558,7 +560,8 @@ def _embed(tokens, embedding, scale, out, row_div, row_mul, row_off):
   ldo = _mat(out, "out")
   _lib.check(_lib.load().cadence_embed(
       _p(tokens), _p(embedding), _p(out), ldo, tokens.numel(),
-      embedding.shape[1], float(scale), row_div, row_mul, row_off,
+      embedding.shape[1], embedding.shape[0], float(scale), row_div, row_mul,
+      row_off,
       _s(tokens)), "embed")
 
 
@@ -739,7 +742,15 @@ def _local_attention(q, k, v, seg_id, seg_start, B, L, H, hd, window):
   _lib.check(_lib.load().cadence_local_attention(
       _p(q), _p(k), _p(v), _p(seg_id), _p(seg_start), _p(out), B, L, H, hd,
       window, _s(q)), "local_attention")
-  TIMER.stop(ev, "flash_attn_kernel<256,0>", 4.0 * B * H * L * L * hd / 2, q)
+  if ev is not None:
+    # algorithmic work = the visible (query, key) pairs only: 4 * H * hd
+    # FLOP each (QK^T and PV), the segment / causal / window mask applied
+    idx = torch.arange(L, device=q.device, dtype=torch.int64)
+    lo = torch.maximum(seg_start.view(B, L).long(), idx - window)
+    pairs = (idx - lo + 1).sum()
+    key = ("griffin_attn_kernel<256>" if hd == 256 and H <= 10 else
+           f"flash_attn_kernel<{hd},0>")
+    TIMER.stop(ev, key, pairs.double() * (4.0 * H * hd), q)
   return out
 
 

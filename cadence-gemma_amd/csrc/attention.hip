@@ -21,6 +21,12 @@
 
 int vit_attention_lds_launch(const void* qkv, void* out, int64_t B, int64_t N,
                              int64_t H, int64_t hd, void* stream);  // vit_attention.hip
+int griffin_attention_launch(const void* q, const void* k, const void* v,
+                             const int32_t* seg_start, void* out, int64_t B,
+                             int64_t L, int64_t H, int64_t hd, int64_t window,
+                             void* stream);  // griffin_attention.hip
+int vit_stream_attention_launch(const void* qkv, void* out, int64_t B, int64_t N,
+                                int64_t H, int64_t hd, void* stream);
 
 namespace {
 
@@ -713,6 +719,13 @@ int cadence_local_attention(const void* q, const void* k, const void* v,
                             int64_t hd, int64_t window, void* stream) {
   if (hd != 256 && hd != 128 && hd != 64) return (int)hipErrorInvalidValue;
   if (B <= 0 || L <= 0) return 0;
+  // MQA workgroups (all heads per K/V tile, griffin_attention.hip) where
+  // they apply; the per-head streaming kernel otherwise
+  {
+    const int rc = griffin_attention_launch(q, k, v, seg_start, out, B, L, H,
+                                            hd, window, stream);
+    if (rc >= 0) return rc;
+  }
   AttnArgs a{};
   a.q = static_cast<const u16*>(q); a.q_bs = L * H * hd; a.q_rs = H * hd; a.q_hs = hd;
   a.k = static_cast<const u16*>(k); a.k_bs = L * hd; a.k_rs = hd; a.k_hs = 0;
@@ -735,6 +748,11 @@ int cadence_vit_attention(const void* qkv, void* out, int64_t B, int64_t N,
   // LDS-resident swapped-QK^T kernel (vit_attention.hip) for short sequences
   {
     const int rc = vit_attention_lds_launch(qkv, out, B, N, H, hd, stream);
+    if (rc >= 0) return rc;
+  }
+  // longer sequences (336 / 384 px towers): K/V tiles streamed by LDS-DMA
+  {
+    const int rc = vit_stream_attention_launch(qkv, out, B, N, H, hd, stream);
     if (rc >= 0) return rc;
   }
   const int64_t D = H * hd;

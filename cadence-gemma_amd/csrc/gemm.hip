@@ -977,6 +977,15 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
   }
 }
 
+// torch.argmax order: NaN beats every number, ties (and NaN vs NaN) go to
+// the lowest index -- a NaN row still yields an index inside the vocabulary
+CADENCE_DEV bool argmax_better(float ov, int oi, float v, int i) {
+  const bool on = ov != ov, n = v != v;
+  if (on != n) return on;
+  if (!on && ov != v) return ov > v;
+  return oi < i;
+}
+
 // ---------------------------------------------------------- skinny engine
 
 // One block: 64 output columns x MS rows over one K split; 4 waves split the
@@ -1063,7 +1072,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(
       for (int off = 32; off > 0; off >>= 1) {
         const float ov = __shfl_xor(v, off, 64);
         const int oi = __shfl_xor(ix, off, 64);
-        if (ov > v || (ov == v && oi < ix)) { v = ov; ix = oi; }
+        if (argmax_better(ov, oi, v, ix)) { v = ov; ix = oi; }
       }
       if (n == 0) {
         bval[(int64_t)m * gridDim.x + blockIdx.x] = v;
@@ -1141,14 +1150,14 @@ __global__ __launch_bounds__(256) void logits_reduce_kernel(
   for (int off = 32; off > 0; off >>= 1) {
     const float ov = __shfl_xor(v, off, 64);
     const int oi = __shfl_xor(idx, off, 64);
-    if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+    if (argmax_better(ov, oi, v, idx)) { v = ov; idx = oi; }
   }
   const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { sv[wave] = v; si[wave] = idx; }
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < 4; ++w)
-      if (sv[w] > v || (sv[w] == v && si[w] < idx)) { v = sv[w]; idx = si[w]; }
+      if (argmax_better(sv[w], si[w], v, idx)) { v = sv[w]; idx = si[w]; }
     bval[(int64_t)m * gridDim.x + blockIdx.x] = v;
     bidx[(int64_t)m * gridDim.x + blockIdx.x] = idx;
   }
@@ -1165,19 +1174,19 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(
   for (int i = threadIdx.x; i < nblk; i += 256) {
     const float ov = bval[(int64_t)m * nblk + i];
     const int oi = bidx[(int64_t)m * nblk + i];
-    if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+    if (argmax_better(ov, oi, v, idx)) { v = ov; idx = oi; }
   }
   for (int off = 32; off > 0; off >>= 1) {
     const float ov = __shfl_xor(v, off, 64);
     const int oi = __shfl_xor(idx, off, 64);
-    if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+    if (argmax_better(ov, oi, v, idx)) { v = ov; idx = oi; }
   }
   const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { sv[wave] = v; si[wave] = idx; }
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < 4; ++w)
-      if (sv[w] > v || (sv[w] == v && si[w] < idx)) { v = sv[w]; idx = si[w]; }
+      if (argmax_better(sv[w], si[w], v, idx)) { v = sv[w]; idx = si[w]; }
     out[m] = idx;
   }
 }

@@ -179,12 +179,15 @@ __global__ __launch_bounds__(256) void layernorm_kernel(
 
 __global__ __launch_bounds__(256) void embed_kernel(
     const int32_t* __restrict__ tok, const u16* __restrict__ E,
-    u16* __restrict__ out, int64_t ldo, int64_t M, int D, float scale,
-    int64_t div, int64_t mul, int64_t off) {
+    u16* __restrict__ out, int64_t ldo, int64_t M, int D, int64_t V,
+    float scale, int64_t div, int64_t mul, int64_t off) {
   const int lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
-  const u16* src = E + (int64_t)tok[m] * D;
+  // an id outside [0, V) reads row 0 instead of faulting (the reference's
+  // nn.Embedding raises; a device kernel cannot)
+  const int64_t t = tok[m];
+  const u16* src = E + (t >= 0 && t < V ? t : 0) * D;
   u16* dst = out + ((m / div) * mul + (m % div) + off) * ldo;
   for (int c = lane * 8; c < D; c += 512) {
     uint4 v = ld16(src + c);
@@ -347,7 +350,7 @@ int cadence_layernorm(const float* x, int64_t ldx, const void* weight,
 }
 
 int cadence_embed(const int32_t* tokens, const void* E, void* out,
-                  int64_t ldo, int64_t M, int64_t D, float scale,
+                  int64_t ldo, int64_t M, int64_t D, int64_t V, float scale,
                   int64_t row_div, int64_t row_mul, int64_t row_off,
                   void* stream) {
   if (D % 8 || ldo % 8 || row_div <= 0) return (int)hipErrorInvalidValue;
@@ -355,7 +358,7 @@ int cadence_embed(const int32_t* tokens, const void* E, void* out,
   hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), tokens,
                      static_cast<const u16*>(E), static_cast<u16*>(out), ldo, M,
-                     (int)D, scale, row_div, row_mul, row_off);
+                     (int)D, V, scale, row_div, row_mul, row_off);
   return (int)hipGetLastError();
 }
 

@@ -209,9 +209,10 @@ int cadence_layernorm(const float* x, int64_t ldx, const void* weight,
                       int64_t width, float eps, void* stream);
 
 /* Embedder.encode (modules.py:994-1001): out[map(m)] = E[tok[m]] * scale
- * (scale = bf16(sqrt(width)) or 1), row remap as in cadence_gemm_linear. */
+ * (scale = bf16(sqrt(width)) or 1), row remap as in cadence_gemm_linear.
+ * E is [V, D]; an id outside [0, V) reads row 0 (no fault). */
 int cadence_embed(const int32_t* tokens, const void* E, void* out,
-                  int64_t ldo, int64_t M, int64_t D, float scale,
+                  int64_t ldo, int64_t M, int64_t D, int64_t V, float scale,
                   int64_t row_div, int64_t row_mul, int64_t row_off,
                   void* stream);
 

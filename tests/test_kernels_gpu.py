@@ -436,8 +436,12 @@ def test_kv_cache_fill_and_decode(dev):
       assert torch.equal(nt.cpu(), ntr.to(torch.int32))
 
 
-@pytest.mark.parametrize("n,h,hd", [(261, 16, 64), (256, 16, 72), (40, 2, 72)])
+@pytest.mark.parametrize("n,h,hd", [(261, 16, 64), (256, 16, 72), (40, 2, 72),
+                                    (581, 16, 64), (576, 16, 72), (734, 16, 64),
+                                    (729, 16, 72), (300, 3, 72), (289, 2, 64)])
 def test_vit_attention(dev, n, h, hd):
+  """timm SDPA (fp32) vs the LDS-resident kernel (N <= 288) and the
+  streaming kernel (336 / 384 px towers: DINO 581 / 734, SigLIP 576 / 729)."""
   g = torch.Generator().manual_seed(11)
   b = 2
   qkv = rnd(b * n, 3 * h * hd, gen=g)

@@ -1,5 +1,6 @@
 """ViT attention microbenchmark at the bench shapes (bs=32, 224 px): DINO
-(N=261, 16 heads x 64) and SigLIP (N=256, 16 x 72).  Reports device
+(N=261, 16 heads x 64) and SigLIP (N=256, 16 x 72), and the 336 / 384 px
+towers (N = 581 / 576, 734 / 729) on the streaming kernel.  Reports device
 time per launch (graph-captured), MFMA TFLOP/s (4*B*H*N^2*hd) and HBM GB/s
 of the algorithmic bytes (qkv in + out)."""
 import os, sys
@@ -23,9 +24,11 @@ def timeit(fn, reps=20):
 
 def main():
   dev = torch.device("cuda")
-  tag = os.environ.get("CADENCE_VIT_ATTN", "lds")
   b = int(os.environ.get("B", "32"))
-  for name, n, h, hd in (("dino", 261, 16, 64), ("siglip", 256, 16, 72)):
+  for name, n, h, hd in (("dino", 261, 16, 64), ("siglip", 256, 16, 72),
+                         ("dino336", 581, 16, 64), ("sig336", 576, 16, 72),
+                         ("dino384", 734, 16, 64), ("sig384", 729, 16, 72)):
+    tag = "lds" if n <= 288 else "stream"
     qkv = torch.randn(b * n, 3 * h * hd, device=dev).to(torch.bfloat16)
     t = qkv.float().view(b, n, 3, h, hd).permute(2, 0, 3, 1, 4)
     att = torch.softmax((t[0] * hd ** -0.5) @ t[1].transpose(-1, -2), -1)
