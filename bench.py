@@ -329,6 +329,8 @@ def main():
   images = None if img_cpu is None else img_cpu.to(dev)
   lengths = torch.full((args.batch,), args.prompt, dtype=torch.int32)
   sampler = cadence.Sampler(model, BenchVocab(), use_graph=True)
+  positions = torch.arange(args.prompt, dtype=torch.int32, device=dev)[None].repeat(
+      args.batch, 1)
 
   def step(events=None):
     outs = []
@@ -338,11 +340,19 @@ def main():
         ev["prefill_start"] = torch.cuda.Event(enable_timing=True)
         ev["prefill_end"] = torch.cuda.Event(enable_timing=True)
         ev["prefill_start"].record()
-      st = sampler.generate(tokens[sl], lengths, args.decode,
-                            images=None if images is None else images[sl],
+      img = None if images is None else images[sl]
+      if args.decode == 0:
+        # prefill only (C4): the forward over [image | prompt] that builds
+        # the caches (Sampler.generate with 0 steps would skip it, as the
+        # reference's return_logits=False / return_cache=False forward does)
+        _, cache = model(tokens[sl], positions, images=img,
+                         return_logits=False, return_cache=True)
+        if ev is not None:
+          ev["prefill_end"].record()
+        outs.append(cache["blocks.0"][0][:, :1].float().to(torch.int32))
+        continue
+      st = sampler.generate(tokens[sl], lengths, args.decode, images=img,
                             events=ev)
-      if args.decode == 0 and ev is not None:
-        ev["prefill_end"].record()
       outs.append(st.tokens_buffer)
     return D.gather_rows(torch.cat(outs))
 

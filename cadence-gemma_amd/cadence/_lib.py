@@ -76,6 +76,9 @@ _SIGS: dict[str, list] = {
     "cadence_resize_bicubic": [P, I64, P, I64, I64, I64, I64, I64, P, P, I64, P,
                                P],
     "cadence_splice_positions": [P, P, I64, I64, I64, P],
+    "cadence_local_attention_cached": [P, P, P, P, P, P, P, I64, I64, I64, I64,
+                                       I64, P],
+    "cadence_kv_ring_update": [P, P, P, P, P, I64, I64, I64, P],
     "cadence_decode_advance": [P, P, I64, P, P, P, P, I32, I32, I64, P],
 }
 _RESTYPE = {

@@ -141,6 +141,18 @@ def rnn_param_init(tensor: torch.Tensor, min_rad: float, max_rad: float,
     return tensor.neg_().exp_().sub_(1.0).log_()   # softplus^-1(-log |A|)
 
 
+def _block_diag_groups(w: torch.Tensor, g: int) -> torch.Tensor:
+  """[H, bw, bw] -> [H / g, g bw, g bw]: each group of g blocks on the
+  diagonal of one zero matrix."""
+  if g == 1:
+    return w
+  h, bw, _ = w.shape
+  out = torch.zeros(h // g, g * bw, g * bw, dtype=w.dtype, device=w.device)
+  for i in range(g):
+    out[:, i * bw:(i + 1) * bw, i * bw:(i + 1) * bw] = w.view(h // g, g, bw, bw)[:, i]
+  return out
+
+
 class RGLRU(nn.Module):
   """Real-Gated Linear Recurrent Unit."""
 
@@ -166,12 +178,28 @@ class RGLRU(nn.Module):
   def a_param_init(self, w: torch.Tensor) -> torch.Tensor:
     return rnn_param_init(w, min_rad=0.9, max_rad=0.999)
 
+  def gate_blocks(self) -> int:
+    """Heads merged into one block of the gate GEMM.  The grouped GEMM tiles
+    64 columns per block; narrower heads (the reference grid's width 128 x
+    16 heads: 8 wide) are merged G at a time into block-diagonal super-blocks
+    whose off-diagonal weights are zero -- the sums are the same (a zero
+    product adds exactly 0), so nothing is approximated."""
+    h, bw = self.num_heads, self.width // self.num_heads
+    for g in range(1, h + 1):
+      if h % g == 0 and (g * bw) % 64 == 0:
+        return g
+    raise NotImplementedError(
+        f"RG-LRU width {self.width} with {h} heads: no head grouping gives a "
+        "block width that is a multiple of 64")
+
   def packed(self):
-    """(W [H, 2*bw, bw] interleaved per 32 rows, bias_x, bias_a, softplus(a))."""
+    """(W [H', 2*bw', bw'] interleaved per 32 rows, bias_x, bias_a,
+    softplus(a)); H' = H / G super-blocks of bw' = G * bw (gate_blocks)."""
     def build():
-      h, bw = self.num_heads, self.width // self.num_heads
-      wx = self.input_gate.w.transpose(1, 2)          # [H, out, in]
-      wa = self.a_gate.w.transpose(1, 2)
+      g = self.gate_blocks()
+      h, bw = self.num_heads // g, g * (self.width // self.num_heads)
+      wx = _block_diag_groups(self.input_gate.w, g).transpose(1, 2)   # [H', out, in]
+      wa = _block_diag_groups(self.a_gate.w, g).transpose(1, 2)
       w = torch.stack([wx.reshape(h, bw // 32, 32, bw),
                        wa.reshape(h, bw // 32, 32, bw)], dim=2)
       w = w.reshape(h, 2 * bw, bw).contiguous()

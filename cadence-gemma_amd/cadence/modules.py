@@ -94,30 +94,37 @@ class LocalAttentionBlock(nn.Module):
         self.final_w_init_variance_scale / self.width))
 
   def qkv_weight(self):
+    """[proj_q; proj_k; proj_v], zero rows appended up to a multiple of 64
+    (the GEMM engines tile 64 columns; only narrow heads need them)."""
+    def build():
+      w = torch.cat([self.proj_q.weight, self.proj_k.weight, self.proj_v.weight])
+      pad = (-w.shape[0]) % 64
+      if pad:
+        w = torch.cat([w, w.new_zeros(pad, w.shape[1])])
+      return w.contiguous()
     return self._packed.get(
-        [self.proj_q.weight, self.proj_k.weight, self.proj_v.weight],
-        lambda: torch.cat([self.proj_q.weight, self.proj_k.weight,
-                           self.proj_v.weight]).contiguous())
+        [self.proj_q.weight, self.proj_k.weight, self.proj_v.weight], build)
 
   def qkv_weight_rope(self):
     """[proj_q; proj_k; proj_v] in cadence_qkv_rope_decode's row order."""
     return self._packed_rope.get(
         [self.proj_q.weight, self.proj_k.weight, self.proj_v.weight],
-        lambda: self.qkv_weight()[ops.qkv_rope_permutation(
+        lambda: self.qkv_weight()[:(self.num_heads + 2) * self.head_dim][ops.qkv_rope_permutation(
             self.num_heads, self.head_dim, self.proj_q.weight.device)].contiguous())
 
   def fused(self, xn2d, pos, b, t, cache, return_cache, resid2d, norm=None):
     """Attention branch on normalised rows; returns (resid + out,
     norm(resid + out) or None, cache)."""
     h, hd = self.num_heads, self.head_dim
-    if cache is not None and t == 1 and b <= 32 and self.width <= 2560:
+    tuned = hd in (64, 128, 256)
+    if cache is not None and t == 1 and b <= 32 and self.width <= 2560 and tuned:
       # decode: RoPE runs in the q|k|v projection's epilogue
       q, k, v = ops.qkv_rope_decode(xn2d, self.qkv_weight_rope(),
                                     pos.view(-1).to(torch.int32), h, hd)
     else:
-      qkv = ops.linear(xn2d, self.qkv_weight())
+      qkv = ops.linear(xn2d, self.qkv_weight())[:, :(h + 2) * hd]
       q, k, v = ops.ops.rope_qkv(qkv, pos.view(-1), h, hd,
-                                 ops.rope_table(qkv.device, hd))
+                                 ops.rope_table(qkv.device, hd) if tuned else None)
     if cache is None:
       # every attention block of a forward sees the same positions tensor:
       # its segment ids / starts are computed once and kept on it
@@ -133,12 +140,30 @@ class LocalAttentionBlock(nn.Module):
         ck, cv, nt = ops.ops.kv_cache_fill(k, v, pos, self.window_size)
         new_cache = AttentionBlockCache(ck, cv, nt)
     else:
-      if t != 1:
+      n_fill = min(self.window_size, t)
+      if n_fill != 1 and n_fill != self.window_size:
         # reference modules.py:206-225 only supports 1 or >= window tokens
         raise NotImplementedError()
-      enc = ops.local_attention_decode_(q, k, v, cache.keys, cache.values,
-                                        cache.num_tokens, h)
-      new_cache = cache if return_cache else None
+      if t == 1 and tuned:
+        enc = ops.local_attention_decode_(q, k, v, cache.keys, cache.values,
+                                          cache.num_tokens, h)
+        new_cache = cache if return_cache else None
+      else:
+        # a multi-token step against the cache (the prompt-in-chunks path,
+        # n_fill == window) or a head dim the tuned decode kernel does not
+        # cover: keys = [ring | new rows], mask from num_tokens
+        enc = ops.ops.local_attention_cached(
+            q, k, v, cache.keys, cache.values, cache.num_tokens, b, t, h, hd,
+            self.window_size)
+        new_cache = None
+        if return_cache:
+          if t == 1:      # in place, as the reference's n_fill == 1 branch
+            ops.ops.kv_ring_update_(k, v, cache.keys, cache.values,
+                                    cache.num_tokens, self.window_size)
+            new_cache = cache
+          else:           # _attention_cache_from_prompt of the new rows
+            ck, cv, nt = ops.ops.kv_cache_fill(k, v, pos, self.window_size)
+            new_cache = AttentionBlockCache(ck, cv, nt)
     out, hn = _out_proj(enc, self.proj_final, resid2d, norm)
     return out, hn, new_cache
 

@@ -768,6 +768,35 @@ def _kv_cache_fill(k, v, segment_pos, window):
   return ck, cv, nt
 
 
+@_reg("local_attention_cached(Tensor q, Tensor k, Tensor v, Tensor cache_k, "
+      "Tensor cache_v, Tensor num_tokens, int B, int T, int H, int hd, "
+      "int window) -> Tensor")
+def _local_attention_cached(q, k, v, cache_k, cache_v, num_tokens, B, T, H, hd,
+                            window):
+  """T query rows against [cache ring | T new keys] (cache-mask semantics,
+  modules.py:155-185); the caches are read, not updated."""
+  for t in (q, k, v, cache_k, cache_v):
+    _need(t.is_contiguous() and t.dtype == _BF16, "q/k/v/caches contiguous bf16")
+  _need(num_tokens.dtype == _I32, "num_tokens int32")
+  out = torch.empty(B * T, H * hd, dtype=_BF16, device=q.device)
+  _lib.check(_lib.load().cadence_local_attention_cached(
+      _p(q), _p(k), _p(v), _p(cache_k), _p(cache_v), _p(num_tokens), _p(out),
+      B, T, H, hd, window, _s(q)), "local_attention_cached")
+  return out
+
+
+@_reg("kv_ring_update_(Tensor k, Tensor v, Tensor(a!) cache_k, "
+      "Tensor(b!) cache_v, Tensor(c!) num_tokens, int window) -> ()")
+def _kv_ring_update(k, v, cache_k, cache_v, num_tokens, window):
+  B = num_tokens.numel()
+  hd = k.shape[-1]
+  _need(k.is_contiguous() and v.is_contiguous(), "k/v contiguous")
+  _need(cache_k.is_contiguous() and cache_v.is_contiguous(), "cache layout")
+  _lib.check(_lib.load().cadence_kv_ring_update(
+      _p(k), _p(v), _p(cache_k), _p(cache_v), _p(num_tokens), B, hd, window,
+      _s(k)), "kv_ring_update")
+
+
 @_reg("local_attention_decode_(Tensor q, Tensor k_new, Tensor v_new, "
       "Tensor(a!) cache_k, Tensor(b!) cache_v, Tensor(c!) num_tokens, int H, "
       "bool out_packed=False) -> Tensor")

@@ -27,6 +27,14 @@ int griffin_attention_launch(const void* q, const void* k, const void* v,
                              void* stream);  // griffin_attention.hip
 int vit_stream_attention_launch(const void* qkv, void* out, int64_t B, int64_t N,
                                 int64_t H, int64_t hd, void* stream);
+int generic_attention_launch(const void* q, const void* k, const void* v,
+                             const void* cache_k, const void* cache_v,
+                             const int32_t* num_tokens, const int32_t* seg_start,
+                             void* out, int64_t B, int64_t T, int64_t H,
+                             int64_t hd, int64_t window, void* stream);
+int rope_qkv_generic_launch(const void* qkv, int64_t ld, const int32_t* positions,
+                            void* q_out, void* k_out, void* v_out, int64_t M,
+                            int64_t H, int64_t hd, void* stream);  // attention_generic.hip
 
 namespace {
 
@@ -692,7 +700,10 @@ int cadence_rope_qkv(const void* qkv, int64_t ldqkv, const int32_t* positions,
                      void* q_out, void* k_out, void* v_out, int64_t M,
                      int64_t H, int64_t hd, const void* table,
                      int64_t table_len, void* stream) {
-  if (hd % 64 || ldqkv % 8) return (int)hipErrorInvalidValue;
+  if (hd % 64)   // head dims the vectorised kernel does not tile
+    return rope_qkv_generic_launch(qkv, ldqkv, positions, q_out, k_out, v_out,
+                                   M, H, hd, stream);
+  if (ldqkv % 8) return (int)hipErrorInvalidValue;
   if (M <= 0) return 0;
   const int cpq = (int)(hd / 4 / 8);
   hipLaunchKernelGGL(rope_qkv_kernel, dim3(grid_cap(M * (H + 1) * cpq)), dim3(256),
@@ -717,7 +728,9 @@ int cadence_local_attention(const void* q, const void* k, const void* v,
                             const int32_t* seg_id, const int32_t* seg_start,
                             void* out, int64_t B, int64_t L, int64_t H,
                             int64_t hd, int64_t window, void* stream) {
-  if (hd != 256 && hd != 128 && hd != 64) return (int)hipErrorInvalidValue;
+  if (hd != 256 && hd != 128 && hd != 64)      // any other head dim
+    return generic_attention_launch(q, k, v, nullptr, nullptr, nullptr,
+                                    seg_start, out, B, L, H, hd, window, stream);
   if (B <= 0 || L <= 0) return 0;
   // MQA workgroups (all heads per K/V tile, griffin_attention.hip) where
   // they apply; the per-head streaming kernel otherwise

@@ -373,6 +373,27 @@ int cadence_splice_positions(const int32_t* text_pos, int32_t* out,
                              int64_t B, int64_t T, int64_t n_vis,
                              void* stream);
 
+/* Local attention of T query rows against [cache ring | T new keys] with
+ * the cache-mask semantics of modules.py:155-185 (positions from
+ * num_tokens, no segment ids): the multi-token cached step of
+ * modules.py:206-225 (n_fill == window) and the single-token step for head
+ * dims the tuned decode kernel does not cover.  Any hd % 4 == 0, hd <= 1024,
+ * window + T <= 6144.  Reads the caches only (update them with
+ * cadence_kv_cache_fill / cadence_kv_ring_update).  q [B*T, H*hd], k_new /
+ * v_new [B*T, hd], cache_k / cache_v [B, window, hd], out [B*T, H*hd]. */
+int cadence_local_attention_cached(const void* q, const void* k_new,
+                                   const void* v_new, const void* cache_k,
+                                   const void* cache_v,
+                                   const int32_t* num_tokens, void* out,
+                                   int64_t B, int64_t T, int64_t H, int64_t hd,
+                                   int64_t window, void* stream);
+
+/* Single-token ring update (modules.py:206-215): slot num_tokens[b] % window
+ * <- k_new[b] / v_new[b]; num_tokens[b] += 1. */
+int cadence_kv_ring_update(const void* k_new, const void* v_new, void* cache_k,
+                           void* cache_v, int32_t* num_tokens, int64_t B,
+                           int64_t hd, int64_t window, void* stream);
+
 /* Greedy decode bookkeeping (the host loop of examples/cadence_sampler.py:
  * 131-151 and the done test of recurrentgemma/torch/sampler.py:217-223
  * moved on device): tokens_out[b, *step] = next_token[b], or pad_id once

@@ -221,15 +221,22 @@ def local_attention(x, segment_pos, p, prefix, num_heads, window, cache=None):
     allk = torch.cat([cache["keys"], k], dim=1)
     allv = torch.cat([cache["values"], v], dim=1)
     mask = cache_mask(t, cache["num_tokens"], window)
-    # modules.py:188-218: single-token decode writes the ring slot in place.
-    assert t == 1, "only seq_len == 1 decode (modules.py:206-225)"
-    slot = cache["num_tokens"] % window
-    nk, nv = cache["keys"].clone(), cache["values"].clone()
-    for i in range(b):
-      nk[i, int(slot[i])] = k[i, 0]
-      nv[i, int(slot[i])] = v[i, 0]
-    new_cache = dict(keys=nk, values=nv,
-                     num_tokens=(cache["num_tokens"] + 1).to(torch.int32))
+    # modules.py:188-225 (_update_attention_cache): n_fill = min(window, t)
+    n_fill = min(window, t)
+    if n_fill == 1:
+      # single-token decode writes the ring slot in place
+      slot = cache["num_tokens"] % window
+      nk, nv = cache["keys"].clone(), cache["values"].clone()
+      for i in range(b):
+        nk[i, int(slot[i])] = k[i, 0]
+        nv[i, int(slot[i])] = v[i, 0]
+      new_cache = dict(keys=nk, values=nv,
+                       num_tokens=(cache["num_tokens"] + 1).to(torch.int32))
+    elif n_fill == window:
+      # prompt in chunks: a fresh cache from the new rows only
+      new_cache = cache_from_prompt(k, v, segment_pos, window)
+    else:
+      raise NotImplementedError("modules.py:224-225")
   else:
     allk, allv = k, v
     mask = prefill_mask(segment_pos, window)
