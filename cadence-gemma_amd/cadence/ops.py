@@ -738,20 +738,32 @@ def _local_attention(q, k, v, seg_id, seg_start, B, L, H, hd, window):
   for t in (q, k, v):
     _need(t.is_contiguous() and t.dtype == _BF16, "q/k/v contiguous bf16")
   out = torch.empty(B * L, H * hd, dtype=_BF16, device=q.device)
+  work = None
+  if TIMER.enabled and not torch.cuda.is_current_stream_capturing():
+    # algorithmic work = the visible (query, key) pairs only: 4 * H * hd
+    # FLOP each (QK^T and PV), the segment / causal / window mask applied;
+    # a device scalar computed outside the timed window, once per positions
+    # tensor (every attention block of a forward shares it)
+    pairs = _visible_pairs.get((seg_start.data_ptr(), window))
+    if pairs is None:
+      idx = torch.arange(L, device=q.device, dtype=torch.int64)
+      lo = torch.maximum(seg_start.view(B, L).long(), idx - window)
+      pairs = (idx - lo + 1).sum().double()
+      _visible_pairs.clear()
+      _visible_pairs[(seg_start.data_ptr(), window)] = pairs
+    work = pairs * (4.0 * H * hd)
   ev = TIMER.start(q)
   _lib.check(_lib.load().cadence_local_attention(
       _p(q), _p(k), _p(v), _p(seg_id), _p(seg_start), _p(out), B, L, H, hd,
       window, _s(q)), "local_attention")
   if ev is not None:
-    # algorithmic work = the visible (query, key) pairs only: 4 * H * hd
-    # FLOP each (QK^T and PV), the segment / causal / window mask applied
-    idx = torch.arange(L, device=q.device, dtype=torch.int64)
-    lo = torch.maximum(seg_start.view(B, L).long(), idx - window)
-    pairs = (idx - lo + 1).sum()
     key = ("griffin_attn_kernel<256>" if hd == 256 and H <= 10 else
            f"flash_attn_kernel<{hd},0>")
-    TIMER.stop(ev, key, pairs.double() * (4.0 * H * hd), q)
+    TIMER.stop(ev, key, work, q)
   return out
+
+
+_visible_pairs: dict = {}
 
 
 @_reg("kv_cache_fill(Tensor k, Tensor v, Tensor segment_pos, int window) -> "
