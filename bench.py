@@ -346,7 +346,8 @@ def main():
         # the caches (Sampler.generate with 0 steps would skip it, as the
         # reference's return_logits=False / return_cache=False forward does)
         _, cache = model(tokens[sl], positions, images=img,
-                         return_logits=False, return_cache=True)
+                         return_logits=False, return_cache=True,
+                         image_splice=img is not None)
         if ev is not None:
           ev["prefill_end"].record()
         outs.append(cache["blocks.0"][0][:, :1].float().to(torch.int32))

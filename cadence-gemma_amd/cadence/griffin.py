@@ -85,8 +85,13 @@ class Griffin(nn.Module):
       raise ValueError(f"{px.shape[0]} images for a batch of {batch}")
     return px.expand(batch, -1, -1, -1).contiguous()   # reference: one image
 
-  def embed_inputs(self, tokens, segment_pos, images=None, img_path=None):
-    """Returns (x [B*L, D], positions [B, L] int32, L) with the image spliced."""
+  def embed_inputs(self, tokens, segment_pos, images=None, img_path=None,
+                   image_splice=None):
+    """Returns (x [B*L, D], positions [B, L] int32, L) with the image spliced.
+
+    `image_splice` (host bool) is the caller's answer to griffin.py:179's
+    "does the prompt hold a position 0" when it knows it without a device
+    sync (the sampler computes positions on the host); None = check here."""
     b, t = tokens.shape
     d = self.config.width
     dev = tokens.device
@@ -95,7 +100,9 @@ class Griffin(nn.Module):
       raise ValueError("images / img_path were given to a Griffin built "
                        "without a vision tower (vision=None)")
     want_image = images is not None or bool(img_path)
-    if want_image and bool((pos == 0).any()):          # griffin.py:179
+    if want_image and image_splice is None:
+      image_splice = bool((pos == 0).any())              # griffin.py:179
+    if want_image and image_splice:
       n_vis = self.n_visual_tokens
       length = n_vis + t
       x = torch.empty(b * length, d, dtype=self.embedder.input_embedding.dtype,
@@ -138,7 +145,8 @@ class Griffin(nn.Module):
   def forward(self, tokens: torch.Tensor, segment_pos: torch.Tensor,
               cache: Cache | None = None, return_logits: bool = True,
               return_cache: bool = True, img_path: str | list[str] | None = None,
-              images: torch.Tensor | None = None):
+              images: torch.Tensor | None = None, *,
+              image_splice: bool | None = None):
     if not return_logits and not return_cache:
       return None, None
     if tokens.ndim == 1:
@@ -146,7 +154,8 @@ class Griffin(nn.Module):
     if segment_pos.ndim == 1:
       segment_pos = segment_pos[None, :]
     b = tokens.shape[0]
-    x, pos, length = self.embed_inputs(tokens, segment_pos, images, img_path)
+    x, pos, length = self.embed_inputs(tokens, segment_pos, images, img_path,
+                                       image_splice)
     x, xn, new_cache = self.run_blocks(x, pos, b, length, cache, return_cache,
                                        final_norm=return_logits)
     if not return_cache:

@@ -80,10 +80,12 @@ class Sampler:
     return self.model.config.vocab_size
 
   def apply_model(self, tokens, segment_pos, cache=None, return_logits=True,
-                  return_cache=True, img_path=None, images=None):
+                  return_cache=True, img_path=None, images=None,
+                  image_splice=None):
     return self.model(tokens=tokens, segment_pos=segment_pos, cache=cache,
                       return_logits=return_logits, return_cache=return_cache,
-                      img_path=img_path, images=images)
+                      img_path=img_path, images=images,
+                      image_splice=image_splice)
 
   def tokenize(self, input_string: str) -> torch.Tensor:
     if self._is_it_model:
@@ -121,15 +123,16 @@ class Sampler:
     # copies only the attention-cache slots the prefill wrote
     n_img = 0
     model_vis = getattr(self.model, "vision_config", None)
-    if (images is not None or img_path) and model_vis is not None and bool(
-        (pos_cpu[:, :-1] == 0).any() if t > 1 else (pos_cpu == 0).any()):
+    splice_all = bool((pos_cpu == 0).any())     # the whole prompt in one call
+    splice = bool((pos_cpu[:, :-1] == 0).any()) if t > 1 else splice_all
+    if (images is not None or img_path) and model_vis is not None and splice:
       n_img = self.model.n_visual_tokens
     tokens = tokens.to(dev, torch.int32)
     steps = total_generation_steps
     if steps == 0:
       prev_logits, _ = self.apply_model(tokens, positions, None,
                                         return_logits and echo, False,
-                                        img_path, images)
+                                        img_path, images, splice_all)
       buf = tokens if echo else torch.empty(b, 0, dtype=torch.int32, device=dev)
       lb = prev_logits[:, -t:] if (return_logits and echo) else None
       return SamplingState(buf, torch.tensor(0), torch.tensor(0), positions,
@@ -147,7 +150,7 @@ class Sampler:
     if t > 1:
       prev_logits, cache = self.apply_model(tokens[:, :-1], positions[:, :-1],
                                             None, return_logits and echo, True,
-                                            img_path, images)
+                                            img_path, images, splice)
       if events is not None:
         events["prefill_end"].record()
       if graph_first:
@@ -168,7 +171,7 @@ class Sampler:
                                             not self.greedy_sampling)
     else:
       logits_all, cache = self.apply_model(tokens, positions, None, True, True,
-                                           img_path, images)
+                                           img_path, images, splice_all)
       logits = logits_all[:, -1]
       nxt = self._sample(logits)
     if not self.greedy_sampling:

@@ -81,7 +81,7 @@ CADENCE_DEV int kswz(int ch, int row) {
 template <int HDK, int HDV, int NPMAX, int NW, int QT, int KW = HDK / 8, int VR = HDV>
 __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
     const u16* __restrict__ qkv, u16* __restrict__ out, int N, int H, int hd,
-    float scale_log2, int dbg) {
+    float scale_log2) {
   constexpr int CPR = KW;             // stored 16-B chunks per K row
   constexpr int KS = HDK / 32;
   constexpr int NDT = HDV / 16;
@@ -118,14 +118,14 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
   const uint4 zero = make_uint4(0, 0, 0, 0);
 
   // K -> LDS, zero-filled past N and past hd
-  for (int c = (dbg == 2 ? 1 << 30 : tid); c < np * CPR; c += NW * 64) {
+  for (int c = tid; c < np * CPR; c += NW * 64) {
     const int key = c / CPR, ch = c % CPR;
     uint4 v = zero;
     if (key < N && ch * 8 < hd) v = ld16(kb + key * rs + ch * 8);
     kimg[key * CPR + kswz<CPR>(ch, key)] = v;
   }
   // V^T -> LDS: one item = 4 keys x 8 dims, written as 8 runs of 4 keys
-  for (int it = (dbg == 2 ? 1 << 30 : tid); it < (np / 4) * VCH; it += NW * 64) {
+  for (int it = tid; it < (np / 4) * VCH; it += NW * 64) {
     const int kq = it / VCH, dc = it % VCH;
     uint4 v[4];
 #pragma unroll
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
   __syncthreads();
 
   const int g = lane >> 4, c16 = lane & 15;
-  const int nqt = dbg == 1 ? 0 : (N + 15) >> 4;
+  const int nqt = (N + 15) >> 4;
   // QT query tiles per pass share every K / V^T fragment read and give the
   // wave QT independent S -> softmax -> PV chains to interleave.
   // Q fragments: unconditional loads from clamped addresses (a branch around
@@ -325,18 +325,6 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
 __attribute__((visibility("hidden"))) int vit_attention_lds_launch(
     const void* qkv, void* out, int64_t B, int64_t N, int64_t H, int64_t hd,
     void* stream) {
-  // CADENCE_VIT_ATTN_CFG = "<waves>x<query tiles>" (A/B sweeps; read once)
-  static const int cfg = [] {
-    const char* e = getenv("CADENCE_VIT_ATTN_CFG");
-    if (!e) return 0;
-    int nw = 0, qt = 0;
-    if (sscanf(e, "%dx%d", &nw, &qt) != 2) return 0;
-    return nw * 10 + qt;
-  }();
-  static const int dbg = [] {   // CADENCE_VIT_ATTN_DBG: 1 staging only, 2 compute only
-    const char* e = getenv("CADENCE_VIT_ATTN_DBG");
-    return e ? atoi(e) : 0;
-  }();
   const float sl2 = 1.4426950408889634f / sqrtf((float)hd);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)H, (unsigned)B);
@@ -344,25 +332,18 @@ __attribute__((visibility("hidden"))) int vit_attention_lds_launch(
   u16* o = static_cast<u16*>(out);
 #define VA(HDK_, HDV_, NP_, NW_, QT_, KW_, VR_)                                       \
   hipLaunchKernelGGL((vit_attn_kernel<HDK_, HDV_, NP_, NW_, QT_, KW_, VR_>), grid,       \
-                     dim3(NW_ * 64), 0, st, in, o, (int)N, (int)H, (int)hd, sl2, dbg)
-#define VSEL(HDK_, HDV_, NP_, KW_, VR_, DEF)                                          \
-  switch (cfg ? cfg : DEF) {                                                          \
-    case 81: VA(HDK_, HDV_, NP_, 8, 1, KW_, VR_); break;                              \
-    default: return -1;                                                               \
-  }
+                     dim3(NW_ * 64), 0, st, in, o, (int)N, (int)H, (int)hd, sl2)
   // 8 waves x 1 query tile (DINO's 17 tiles on 9 waves measured 10 % slower:
   // 18 waves per CU do not split evenly over the 4 SIMDs)
-  const int def = 81;
   if (hd == 64 && N <= 288) {
-    VSEL(64, 64, 288, 8, 64, def)
+    VA(64, 64, 288, 8, 1, 8, 64);
   } else if (hd == 72 && N <= 256) {
-    VSEL(96, 80, 256, 10, 72, def)
+    VA(96, 80, 256, 8, 1, 10, 72);
   } else if (hd == 72 && N <= 288) {
-    VSEL(96, 80, 288, 10, 72, def)
+    VA(96, 80, 288, 8, 1, 10, 72);
   } else {
     return -1;
   }
-#undef VSEL
 #undef VA
   return (int)hipGetLastError();
 }
