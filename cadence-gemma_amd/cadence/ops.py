@@ -614,7 +614,7 @@ def _rnn_scan(x, a, segment_pos, h0, gate, B, L):
   per_elem = 6 + (2 if gate is not None else 0)
   nbytes = (B * L * E * per_elem + B * E * 4 * (2 if h0 is not None else 1)
             + (B * L * 4 if pos is not None else 0))
-  TIMER.stop(ev, "rnn_scan_kernel", nbytes, x)
+  TIMER.stop(ev, "rnn_scan_chunk_kernel" if wsb else "rnn_scan_kernel", nbytes, x)
   return out, h_last
 
 
