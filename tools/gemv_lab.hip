@@ -1,0 +1,164 @@
+// Decode GEMV lab: cold-weight timing of the stream engine's variants on the
+// decode shapes (M = 32 packed rows, fragment-packed weights), each variant
+// captured as a hipGraph of back-to-back launches cycling over enough weight
+// copies that nothing is served from the 256 MB Infinity Cache.  Also a pure
+// streaming-read kernel over the same bytes (the bandwidth this size can
+// reach).  Not part of the library; built by tools/gemv_lab.sh.
+#include "../cadence-gemma_amd/csrc/gemm.hip"
+
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1); } } while (0)
+
+namespace {
+
+__global__ __launch_bounds__(256) void read_kernel(const uint4* __restrict__ p, int64_t n16,
+                                                   uint32_t* __restrict__ sink) {
+  uint32_t acc = 0;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) {
+    const uint4 v = ld16_nt(reinterpret_cast<const u16*>(p + i));
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+struct Lab {
+  hipStream_t st;
+  std::vector<u16*> w;
+  u16* x;
+  float* parts;
+  u16* out;
+  u16* bias;
+  int copies;
+  int64_t wbytes;
+};
+
+template <class F>
+double time_graph(Lab& L, int reps, F&& launch_one) {
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  for (int i = 0; i < 3; ++i) launch_one(i % L.copies);
+  CK(hipStreamSynchronize(L.st));
+  CK(hipStreamBeginCapture(L.st, hipStreamCaptureModeGlobal));
+  for (int i = 0; i < reps; ++i) launch_one(i % L.copies);
+  CK(hipStreamEndCapture(L.st, &g));
+  CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  CK(hipGraphLaunch(ge, L.st));
+  CK(hipStreamSynchronize(L.st));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  double best = 1e30;
+  for (int t = 0; t < 5; ++t) {
+    CK(hipEventRecord(a, L.st));
+    CK(hipGraphLaunch(ge, L.st));
+    CK(hipEventRecord(b, L.st));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    best = std::min(best, (double)ms * 1e3 / reps);
+  }
+  CK(hipGraphExecDestroy(ge));
+  CK(hipGraphDestroy(g));
+  return best;
+}
+
+void report(const char* name, double us, int64_t bytes) {
+  printf("%-58s %8.2f us  %6.2f TB/s\n", name, us, bytes / (us * 1e-6) / 1e12);
+  fflush(stdout);
+}
+
+template <int MS, int KSW, int NTW, class Epi>
+void run_stream(Lab& L, const char* name, int N, int K, int splits, const Epi& epi,
+                bool with_reduce) {
+  const int nblk = Epi::kPaired ? N / 32 : N / 16 / NTW;
+  const int ks = K / 32;
+  const int klen = ((ks + splits - 1) / splits) * 32;
+  const int need_steps = (klen / 32 + 7) / 8;
+  if (need_steps > KSW) { printf("%-58s skipped (KSW too small)\n", name); return; }
+  dim3 grid(nblk, splits, 1);
+  float* parts = splits > 1 ? L.parts : nullptr;
+  const double us = time_graph(L, 60, [&](int c) {
+    hipLaunchKernelGGL((gemm_stream_kernel<MS, KSW, NTW, Epi>), grid, dim3(512), 0, L.st,
+                       L.x, (int64_t)0, L.w[c], (int64_t)0, 32, N, K, klen, (int64_t)0,
+                       (int64_t)0, parts, epi, 1);
+    if (with_reduce && splits > 1) {
+      int rb = (32 * N + 255) / 256;
+      hipLaunchKernelGGL((splitk_reduce_kernel<Epi>), dim3(rb, 1), dim3(256), 0, L.st,
+                         parts, splits, 1, 32, N, epi);
+    }
+  });
+  report(name, us, (int64_t)N * K * 2);
+}
+
+void run_read(Lab& L, const char* name, int64_t bytes, int blocks) {
+  const double us = time_graph(L, 60, [&](int c) {
+    hipLaunchKernelGGL(read_kernel, dim3(blocks), dim3(256), 0, L.st,
+                       reinterpret_cast<const uint4*>(L.w[c]), bytes / 16,
+                       reinterpret_cast<uint32_t*>(L.out));
+  });
+  report(name, us, bytes);
+}
+
+}  // namespace
+
+int main() {
+  Lab L;
+  CK(hipStreamCreate(&L.st));
+  L.wbytes = (int64_t)15360 * 2560 * 2;     // largest shape: gated up-projection
+  L.copies = 8;                              // 8 x 78.6 MB > 256 MB MALL
+  for (int i = 0; i < L.copies; ++i) {
+    u16* p;
+    CK(hipMalloc(&p, L.wbytes));
+    CK(hipMemset(p, 0x3c, L.wbytes));
+    L.w.push_back(p);
+  }
+  CK(hipMalloc(&L.x, 32 * 7680 * 2));
+  CK(hipMemset(L.x, 0x3c, 32 * 7680 * 2));
+  CK(hipMalloc(&L.parts, (int64_t)8 * 32 * 15360 * 4));
+  CK(hipMalloc(&L.out, (int64_t)32 * 15360 * 2 * 2));
+  CK(hipMalloc(&L.bias, 15360 * 2));
+  CK(hipMemset(L.bias, 0, 15360 * 2));
+
+  printf("== pure streaming read (nt 16-B loads)\n");
+  for (int64_t mb : {13, 26, 39, 79}) {
+    const int64_t bytes = mb == 13 ? 2560LL * 2560 * 2 : mb == 26 ? 5120LL * 2560 * 2
+                        : mb == 39 ? 2560LL * 7680 * 2 : 15360LL * 2560 * 2;
+    for (int blocks : {512, 1024, 2048}) {
+      char nm[96];
+      snprintf(nm, sizeof nm, "read %lld MB, %d blocks x 256", (long long)(bytes >> 20), blocks);
+      run_read(L, nm, bytes, blocks);
+    }
+  }
+
+  EpiGatedGelu gg{L.out, 0, L.bias, L.bias, 2};
+  printf("== gated up-projection N=15360 (2F) K=2560\n");
+  run_stream<32, 10, 1>(L, "stream<32,10,1,Gated> s1 (shipped)", 15360, 2560, 1, gg, false);
+  run_stream<32, 5, 1>(L, "stream<32,5,1,Gated> s2 raw partials", 15360, 2560, 2, gg, false);
+  run_stream<32, 5, 1>(L, "stream<32,5,1,Gated> s2 + reduce", 15360, 2560, 2, gg, true);
+  run_stream<32, 4, 1>(L, "stream<32,4,1,Gated> s3 raw partials", 15360, 2560, 3, gg, false);
+  run_stream<32, 3, 1>(L, "stream<32,3,1,Gated> s4 raw partials", 15360, 2560, 4, gg, false);
+
+  EpiLinear el{L.out, 0, nullptr, nullptr, 0, 0, RowMap{1 << 30, 0, 0}, 0.f};
+  printf("== down-projection N=2560 K=7680\n");
+  run_stream<32, 10, 2>(L, "stream<32,10,2> s3 raw (shipped)", 2560, 7680, 3, el, false);
+  run_stream<32, 10, 1>(L, "stream<32,10,1> s3 raw", 2560, 7680, 3, el, false);
+  run_stream<32, 5, 2>(L, "stream<32,5,2> s6 raw", 2560, 7680, 6, el, false);
+  run_stream<32, 5, 1>(L, "stream<32,5,1> s6 raw", 2560, 7680, 6, el, false);
+  run_stream<32, 4, 1>(L, "stream<32,4,1> s8 raw", 2560, 7680, 8, el, false);
+  printf("== y|x projection N=5120 K=2560\n");
+  run_stream<32, 10, 2>(L, "stream<32,10,2> s1 (shipped)", 5120, 2560, 1, el, false);
+  run_stream<32, 10, 1>(L, "stream<32,10,1> s1", 5120, 2560, 1, el, false);
+  run_stream<32, 5, 2>(L, "stream<32,5,2> s2 raw", 5120, 2560, 2, el, false);
+  run_stream<32, 5, 1>(L, "stream<32,5,1> s2 raw", 5120, 2560, 2, el, false);
+  run_stream<32, 4, 1>(L, "stream<32,4,1> s3 raw", 5120, 2560, 3, el, false);
+  printf("== output projection N=2560 K=2560\n");
+  run_stream<32, 5, 2>(L, "stream<32,5,2> s2 raw (shipped)", 2560, 2560, 2, el, false);
+  run_stream<32, 5, 1>(L, "stream<32,5,1> s2 raw", 2560, 2560, 2, el, false);
+  run_stream<32, 10, 1>(L, "stream<32,10,1> s1", 2560, 2560, 1, el, false);
+  run_stream<32, 4, 1>(L, "stream<32,4,1> s3 raw", 2560, 2560, 3, el, false);
+  run_stream<32, 3, 1>(L, "stream<32,3,1> s4 raw", 2560, 2560, 4, el, false);
+  printf("done\n");
+  return 0;
+}
