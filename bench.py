@@ -346,7 +346,10 @@ def main():
   def step(events=None):
     outs = []
     for j, sl in enumerate(micro):
-      ev = events if j == 0 else None
+      # the last micro-batch: by then the host has run ahead of the GPU, so
+      # its prefill events time the GPU, not the launch loop (the first
+      # micro-batch of a step starts on an empty queue)
+      ev = events if j == n_micro - 1 else None
       if args.decode == 0 and ev is not None:    # prefill only (C4)
         ev["prefill_start"] = torch.cuda.Event(enable_timing=True)
         ev["prefill_end"] = torch.cuda.Event(enable_timing=True)

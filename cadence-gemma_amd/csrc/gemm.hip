@@ -37,6 +37,10 @@ namespace {
 
 constexpr int BK = 64;
 
+// 1 KiB of zeros: the stream engine reads a fragment that must be zero from
+// here (one lane-linear 16-B load per lane) instead of masking a loaded one.
+__device__ __attribute__((aligned(16))) uint4 kZeroPage[64] = {};   // never written
+
 // ---------------------------------------------------------------- epilogues
 
 struct RowMap {
@@ -161,16 +165,15 @@ struct EpiLinearConv : EpiLinear {
   int conv_lo, E;
   struct Pref { u16 w[TW], s[TW > 1 ? TW - 1 : 1], b; };
   CADENCE_DEV Pref prefetch(int64_t m, int n) const {
+    // branch-free: y-branch columns read channel 0 (unused)
     Pref p{};
-    if (n >= conv_lo) {
-      const int c = n - conv_lo;
-      const u16* srow = state + m * (int64_t)(TW - 1) * E + c;
+    const int c = n >= conv_lo ? n - conv_lo : 0;
+    const u16* srow = state + m * (int64_t)(TW - 1) * E + c;
 #pragma unroll
-      for (int t = 0; t < TW; ++t) p.w[t] = cw[(int64_t)t * E + c];
+    for (int t = 0; t < TW; ++t) p.w[t] = cw[(int64_t)t * E + c];
 #pragma unroll
-      for (int r = 0; r < TW - 1; ++r) p.s[r] = srow[(int64_t)r * E];
-      p.b = cb[c];
-    }
+    for (int r = 0; r < TW - 1; ++r) p.s[r] = srow[(int64_t)r * E];
+    p.b = cb[c];
     return p;
   }
   CADENCE_DEV void apply_pf(int64_t m, int n, float v, int g, const Pref& p) const {
@@ -271,6 +274,16 @@ struct EpiGatedGelu {
   CADENCE_DEV void apply2(int64_t m, int f, float g, float u, int gg) const {
     out[xoff((int)m, f, ldo, mt)] = f2bf(value2(m, f, g, u, gg));
   }
+  // stream engine: the biases are loaded at kernel start (kPrefetch), so the
+  // epilogue issues no dependent global load after the weight stream
+  static constexpr bool kPrefetch = true;
+  struct Pref { u16 bg, bu; };
+  CADENCE_DEV Pref prefetch2(int64_t, int f, int) const { return Pref{bias_g[f], bias_u[f]}; }
+  CADENCE_DEV void apply2_pf(int64_t m, int f, float g, float u, int, const Pref& p) const {
+    g = badd(rbf(g), bf2f(p.bg));
+    u = badd(rbf(u), bf2f(p.bu));
+    out[xoff((int)m, f, ldo, mt)] = f2bf(bmul(rbf(gelu_tanh(g)), u));
+  }
   CADENCE_DEV float bias_at(bool up, int f, int) const {
     return bf2f((up ? bias_u : bias_g)[f]);
   }
@@ -335,6 +348,42 @@ struct EpiRglruGates {
       *hp = hn;
       float y = rbf(hn);
       if (gate) y = bmul(y, bf2f(gate[m * ldg + e]));
+      y_out[xoff((int)m, e, ldy, mt)] = f2bf(y);
+      return;
+    }
+    a_out[m * ldo + e] = f2bf(av);
+    nx_out[m * ldo + e] = f2bf(nx);
+  }
+  // stream engine: every per-element operand is loaded at kernel start
+  // (kPrefetch) and lands while the weight stream is in flight
+  static constexpr bool kPrefetch = true;
+  struct Pref { u16 bx, ba, xv, sp, gt; int reset; float h; };
+  CADENCE_DEV Pref prefetch2(int64_t m, int j, int g) const {
+    const int e = g * bw + j;
+    Pref p;
+    p.bx = bias_x[e];
+    p.ba = bias_a[e];
+    p.xv = x[m * ldx + e];
+    p.sp = softplus_a[e];
+    p.reset = segpos[m] == 0;
+    // branch-free: absent operands read the zero page
+    const float* hp = h ? h + m * ldh + e : reinterpret_cast<const float*>(kZeroPage);
+    const u16* gp = (h && gate) ? gate + m * ldg + e : reinterpret_cast<const u16*>(kZeroPage);
+    p.h = *hp;
+    p.gt = *gp;
+    return p;
+  }
+  CADENCE_DEV void apply2_pf(int64_t m, int j, float accx, float acca, int g,
+                             const Pref& p) const {
+    const int e = g * bw + j;
+    float av, nx;
+    chain(badd(rbf(accx), bf2f(p.bx)), badd(rbf(acca), bf2f(p.ba)), bf2f(p.xv),
+          bf2f(p.sp), p.reset != 0, av, nx);
+    if (h) {
+      const float hn = add_rn(mul_rn(av, p.h), nx);
+      h[m * ldh + e] = hn;
+      float y = rbf(hn);
+      if (gate) y = bmul(y, bf2f(p.gt));
       y_out[xoff((int)m, e, ldy, mt)] = f2bf(y);
       return;
     }
@@ -877,33 +926,47 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
   }
   // prefetching epilogues: this thread's epilogue elements are row tid / 16,
   // columns col[j] + tid % 16 (the epilogue loop below runs once per thread)
+  // (paired: one (gate, up) element per thread, column grp * 32 + half * 16 +
+  // tid % 16 of the epilogue's output)
   constexpr bool kPf = EpiPrefetch<Epi>::value;
   [[maybe_unused]] typename std::conditional<kPf, Epi, EpiLinear>::type::Pref pf[NREP];
+  // (unconditional, rows clamped to M - 1: a load under a branch would cost
+  // a vmcnt(0) at the join before the weight stream is even issued)
   if constexpr (kPf) {
-    static_assert(!Epi::kPaired && MS * 16 <= 512, "one epilogue element per thread");
-    if ((int)threadIdx.x < MS * 16 && (int)(threadIdx.x >> 4) < M && !parts) {
+    static_assert(MS * 16 <= 512, "one epilogue element per thread");
+    const int pm = min((int)(threadIdx.x >> 4), M - 1);
+    if constexpr (Epi::kPaired) {
+      pf[0] = epi.prefetch2(pm, (blockIdx.x >> 1) * 32 + (blockIdx.x & 1) * 16 + (threadIdx.x & 15),
+                            g);
+    } else {
 #pragma unroll
-      for (int j = 0; j < NREP; ++j)
-        pf[j] = epi.prefetch(threadIdx.x >> 4, col[j] + (threadIdx.x & 15));
+      for (int j = 0; j < NREP; ++j) pf[j] = epi.prefetch(pm, col[j] + (threadIdx.x & 15));
     }
   }
   const int koff = 8 * (lane >> 4);
   const int kbeg = blockIdx.y * klen;
   const int kend = min(K, kbeg + klen);
   const uint4 zero = make_uint4(0, 0, 0, 0);
+  // Branch-free issue: every load is unconditional; a fragment that must be
+  // zero (k past the split, rows past M) is read from a zero page instead of
+  // being masked after the load.  A load under a branch makes the waitcnt
+  // pass put a vmcnt(0) at the join, and a select on the loaded value waits
+  // for it: either costs a full memory round trip per k-step instead of one
+  // per workgroup.
+  const u16* zpage = reinterpret_cast<const u16*>(kZeroPage + lane);
   uint4 wb[KSW][NREP], xa[KSW][MR];
 #pragma unroll
   for (int u = 0; u < KSW; ++u) {
     const int k = kbeg + (wave + 8 * u) * 32;
     const bool ok = k < kend;
 #pragma unroll
-    for (int j = 0; j < NREP; ++j)
-      if (packed)   // fragment-packed [N/16][K/32][64 lanes][8]: 1 KiB per load
-        wb[u][j] = ok ? ld16_nt(W + (((int64_t)(col[j] >> 4) * (K >> 5) + (k >> 5)) * 64 + lane) * 8)
-                      : zero;
-      else
-        wb[u][j] = ok ? ld16(W + (int64_t)(col[j] + (lane & 15)) * ldw + k + koff)
-                      : zero;
+    for (int j = 0; j < NREP; ++j) {
+      // fragment-packed [N/16][K/32][64 lanes][8]: 1 KiB per load
+      const int64_t off = packed
+          ? (((int64_t)(col[j] >> 4) * (K >> 5) + (k >> 5)) * 64 + lane) * 8
+          : (int64_t)(col[j] + (lane & 15)) * ldw + k + koff;
+      wb[u][j] = ld16_nt(ok ? W + off : zpage);
+    }
   }
 #pragma unroll
   for (int u = 0; u < KSW; ++u) {
@@ -912,10 +975,10 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
 #pragma unroll
     for (int i = 0; i < MR; ++i) {
       const int m = i * 16 + (lane & 15);
-      if (lda == 0)   // packed rows (common.hpp xpk): mt == MR here
-        xa[u][i] = ok ? ld16(A + ((((int64_t)(k >> 5) * MR + i) * 64 + lane) << 3)) : zero;
-      else
-        xa[u][i] = (ok && m < M) ? ld16(A + (int64_t)m * lda + k + koff) : zero;
+      // packed rows (common.hpp xpk, mt == MR here) or row-major
+      const int64_t off = lda == 0 ? ((((int64_t)(k >> 5) * MR + i) * 64 + lane) << 3)
+                                   : (int64_t)m * lda + k + koff;
+      xa[u][i] = ld16((ok && (lda == 0 || m < M)) ? A + off : zpage);
     }
   }
   f32x4 acc[MR][NREP];
@@ -958,7 +1021,10 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
       for (int j = 0; j < NREP; ++j) dst[col[j] + c] = v[j];
     } else if constexpr (Epi::kPaired) {
       const int grp = blockIdx.x >> 1, half = blockIdx.x & 1;
-      epi.apply2(m, grp * 32 + half * 16 + c, v[0], v[NREP - 1], g);
+      if constexpr (kPf)
+        epi.apply2_pf(m, grp * 32 + half * 16 + c, v[0], v[NREP - 1], g, pf[0]);
+      else
+        epi.apply2(m, grp * 32 + half * 16 + c, v[0], v[NREP - 1], g);
     } else if constexpr (EpiPairLanes<Epi>::value) {
       // lanes o and o ^ 1 hold the two columns of a pair (same row m)
 #pragma unroll

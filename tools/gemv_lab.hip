@@ -23,6 +23,74 @@ __global__ __launch_bounds__(256) void read_kernel(const uint4* __restrict__ p, 
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// Lab copy of the stream engine's core: MODE 0 = weights + packed-row
+// activations (as shipped), 1 = weights only (activation fragments are a
+// constant), 2 = weights only and no MFMA (XOR of the loads).
+template <int KSW, int NREP, int MODE>
+__global__ __launch_bounds__(512) void lab_gemv(const u16* __restrict__ A,
+                                                const u16* __restrict__ W, int N, int K,
+                                                int klen, float* __restrict__ out) {
+  constexpr int MR = 2;
+  __shared__ float red[8][32 * 16 * NREP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kbeg = blockIdx.y * klen, kend = min(K, kbeg + klen);
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  uint4 wb[KSW][NREP], xa[KSW][MR];
+#pragma unroll
+  for (int u = 0; u < KSW; ++u) {
+    const int k = kbeg + (wave + 8 * u) * 32;
+    const bool ok = k < kend;
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      const int col = (blockIdx.x * NREP + j) * 16;
+      wb[u][j] = ok ? ld16_nt(W + (((int64_t)(col >> 4) * (K >> 5) + (k >> 5)) * 64 + lane) * 8)
+                    : zero;
+    }
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+      xa[u][i] = (MODE == 0 && ok) ? ld16(A + ((((int64_t)(k >> 5) * MR + i) * 64 + lane) << 3))
+                                   : make_uint4(0x3c003c00u, 0x3c003c00u, lane, i);
+  }
+  if constexpr (MODE == 2) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < KSW; ++u)
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) acc ^= wb[u][j].x ^ wb[u][j].y ^ wb[u][j].z ^ wb[u][j].w;
+    if (acc == 0x12345678u) out[0] = 1.0f;
+    return;
+  }
+  f32x4 acc[MR][NREP];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < KSW; ++u)
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NREP; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8, xa[u][i]), __builtin_bit_cast(bf16x8, wb[u][j]),
+            acc[i][j], 0, 0, 0);
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[wave][((i * 16 + rsub + r) * NREP + j) * 16 + csub] = acc[i][j][r];
+  __syncthreads();
+  for (int o = threadIdx.x; o < 32 * 16 * NREP; o += 512) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += red[w][o];
+    out[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 32 * 16 * NREP + o] = v;
+  }
+}
+
 struct Lab {
   hipStream_t st;
   std::vector<u16*> w;
@@ -88,6 +156,19 @@ void run_stream(Lab& L, const char* name, int N, int K, int splits, const Epi& e
       hipLaunchKernelGGL((splitk_reduce_kernel<Epi>), dim3(rb, 1), dim3(256), 0, L.st,
                          parts, splits, 1, 32, N, epi);
     }
+  });
+  report(name, us, (int64_t)N * K * 2);
+}
+
+template <int KSW, int NREP, int MODE>
+void run_lab(Lab& L, const char* name, int N, int K, int splits) {
+  const int ks = K / 32;
+  const int klen = ((ks + splits - 1) / splits) * 32;
+  if ((klen / 32 + 7) / 8 > KSW) { printf("%-58s skipped\n", name); return; }
+  dim3 grid(N / 16 / NREP, splits);
+  const double us = time_graph(L, 60, [&](int c) {
+    hipLaunchKernelGGL((lab_gemv<KSW, NREP, MODE>), grid, dim3(512), 0, L.st, L.x, L.w[c],
+                       N, K, klen, L.parts);
   });
   report(name, us, (int64_t)N * K * 2);
 }
@@ -159,6 +240,22 @@ int main() {
   run_stream<32, 10, 1>(L, "stream<32,10,1> s1", 2560, 2560, 1, el, false);
   run_stream<32, 4, 1>(L, "stream<32,4,1> s3 raw", 2560, 2560, 3, el, false);
   run_stream<32, 3, 1>(L, "stream<32,3,1> s4 raw", 2560, 2560, 4, el, false);
+  printf("== lab core, gated shape N=15360 K=2560\n");
+  run_lab<10, 2, 0>(L, "lab<10,2> act+w s1", 15360, 2560, 1);
+  run_lab<10, 2, 1>(L, "lab<10,2> w only s1", 15360, 2560, 1);
+  run_lab<10, 2, 2>(L, "lab<10,2> w only no-mfma s1", 15360, 2560, 1);
+  run_lab<5, 2, 0>(L, "lab<5,2> act+w s2", 15360, 2560, 2);
+  run_lab<5, 2, 1>(L, "lab<5,2> w only s2", 15360, 2560, 2);
+  run_lab<5, 4, 0>(L, "lab<5,4> act+w s2", 15360, 2560, 2);
+  run_lab<5, 4, 1>(L, "lab<5,4> w only s2", 15360, 2560, 2);
+  run_lab<3, 4, 0>(L, "lab<3,4> act+w s4", 15360, 2560, 4);
+  run_lab<2, 4, 0>(L, "lab<2,4> act+w s5", 15360, 2560, 5);
+  run_lab<10, 1, 0>(L, "lab<10,1> act+w s1", 15360, 2560, 1);
+  printf("== lab core, down shape N=2560 K=7680\n");
+  run_lab<10, 2, 0>(L, "lab<10,2> act+w s3", 2560, 7680, 3);
+  run_lab<10, 2, 1>(L, "lab<10,2> w only s3", 2560, 7680, 3);
+  run_lab<5, 4, 0>(L, "lab<5,4> act+w s6", 2560, 7680, 6);
+  run_lab<3, 4, 0>(L, "lab<3,4> act+w s10", 2560, 7680, 10);
   printf("done\n");
   return 0;
 }
