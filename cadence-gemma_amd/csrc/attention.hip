@@ -319,15 +319,16 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
   // slots with a non-negative position: all of them once the ring wrapped
   const int slot_hi = nt >= a.W ? a.W : nt;
 
+  // branch-free loads throughout (absent rows / slots read the zero page)
+  const u16* zpage = reinterpret_cast<const u16*>(kZeroPage + lane);
   bf16x8 qf[KS];
   {
     const int hrow = lane & 15;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int d = ks * 32 + 8 * (lane >> 4);
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (hrow < a.H) v = ld16(a.q + (int64_t)b * a.H * a.hd + hrow * a.hd + d);
-      qf[ks] = __builtin_bit_cast(bf16x8, v);
+      qf[ks] = __builtin_bit_cast(
+          bf16x8, ld16(hrow < a.H ? a.q + (int64_t)b * a.H * a.hd + hrow * a.hd + d : zpage));
     }
   }
   f32x4 o[NO];
@@ -360,14 +361,12 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
       const int c = tid + i * 256;
       const int kr = c / CPR, d = (c % CPR) * 8;
       const int slot = k0 + kr;
-      kreg[i] = vreg[i] = make_uint4(0, 0, 0, 0);
-      if (slot < a.W) {
-        kreg[i] = ld16(ckb + (int64_t)slot * a.hd + d);
-        vreg[i] = ld16(cvb + (int64_t)slot * a.hd + d);
-      } else if (slot == a.W) {
-        kreg[i] = ld16(a.k_new + (int64_t)b * a.new_rs + d);
-        vreg[i] = ld16(a.v_new + (int64_t)b * a.new_rs + d);
-      }
+      const u16* kp = slot < a.W ? ckb + (int64_t)slot * a.hd + d
+                    : slot == a.W ? a.k_new + (int64_t)b * a.new_rs + d : zpage;
+      const u16* vp = slot < a.W ? cvb + (int64_t)slot * a.hd + d
+                    : slot == a.W ? a.v_new + (int64_t)b * a.new_rs + d : zpage;
+      kreg[i] = ld16(kp);
+      vreg[i] = ld16(vp);
     }
   };
   if (tb < te) fetch(tb);

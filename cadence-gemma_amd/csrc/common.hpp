@@ -16,6 +16,14 @@ typedef uint16_t u16;
 
 #define CADENCE_DEV __device__ __forceinline__
 
+namespace {
+// 1 KiB of zeros (never written): a kernel reads a fragment that must be
+// zero from here (lane-linear 16-B loads) instead of loading under a branch
+// or masking a loaded value -- either makes the waitcnt pass serialise a
+// full memory round trip.
+__device__ __attribute__((aligned(16))) uint4 kZeroPage[64] = {};
+}  // namespace
+
 CADENCE_DEV float bf2f(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
 CADENCE_DEV float bf2f(bf16 v) { return (float)v; }
 // Round-to-nearest-even fp32 -> bf16 (v_cvt_pk_bf16_f32 on gfx950; keeps NaN).

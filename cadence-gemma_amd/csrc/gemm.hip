@@ -37,9 +37,6 @@ namespace {
 
 constexpr int BK = 64;
 
-// 1 KiB of zeros: the stream engine reads a fragment that must be zero from
-// here (one lane-linear 16-B load per lane) instead of masking a loaded one.
-__device__ __attribute__((aligned(16))) uint4 kZeroPage[64] = {};   // never written
 
 // ---------------------------------------------------------------- epilogues
 
@@ -1273,8 +1270,12 @@ __global__ __launch_bounds__(512) void reduce_rmsnorm_kernel(
   const int m = blockIdx.x, tid = threadIdx.x;
   const int64_t orow = epi.map(m);
   // issue every load of the row first (S splits x RC chunks, resid, scale)
+  // (bias / residual chunks are read from the zero page when absent: a load
+  // under a branch, or one per element in the epilogue, would serialise a
+  // memory round trip each)
+  const u16* zpage = reinterpret_cast<const u16*>(kZeroPage + (tid & 63));
   float4 pa[RC][S][2];
-  uint4 rq[RC], sq[RC];
+  uint4 rq[RC], sq[RC], bq[RC];
 #pragma unroll
   for (int c = 0; c < RC; ++c) {
     const int n0 = min((tid + c * 512) * 8, N - 8);
@@ -1285,7 +1286,8 @@ __global__ __launch_bounds__(512) void reduce_rmsnorm_kernel(
       pa[c][sp][0] = src[0];
       pa[c][sp][1] = src[1];
     }
-    rq[c] = epi.resid ? ld16(epi.resid + orow * epi.ldr + n0) : make_uint4(0, 0, 0, 0);
+    rq[c] = ld16(epi.resid ? epi.resid + orow * epi.ldr + n0 : zpage);
+    bq[c] = ld16(epi.bias ? epi.bias + n0 : zpage);
     sq[c] = ld16(scale + n0);
   }
   float o[RC][8];
@@ -1301,11 +1303,15 @@ __global__ __launch_bounds__(512) void reduce_rmsnorm_kernel(
         v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
         v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
       }
-      float r[8];
+      float r[8], bb[8];
       unpack8(rq[c], r);
+      unpack8(bq[c], bb);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float y = epi.value(m, n0 + i, v[i], 0);
+        // EpiLinear::value with the bias chunk preloaded
+        float y = v[i];
+        if (epi.bias) y = add_rn(y, bb[i]);
+        y = epi.activate(rbf(y));
         if (epi.resid) y = badd(y, r[i]);
         o[c][i] = y;
         ss += rbf(y * y);
