@@ -42,6 +42,7 @@ constexpr int MODE_LOCAL = 0;
 constexpr int MODE_VIT = 1;
 constexpr int KT = 32;  // keys per tile
 constexpr int kDecodeSplits = 8;  // window splits of the decode attention
+constexpr int kMinTilesPerSplit = 4;  // key tiles per split, at least
 
 struct AttnArgs {
   const u16* q; int64_t q_bs, q_rs, q_hs;   // batch / row / head strides
@@ -347,8 +348,14 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
   const int ring_tiles = (slot_hi + KT - 1) / KT;
   const int last_tile = a.W / KT;
   const int ntot = last_tile < ring_tiles ? ring_tiles : ring_tiles + 1;
-  const int tps = (ntot + NS - 1) / NS;
-  const int tb = min(ntot, split * tps), te = min(ntot, tb + tps);
+  // at least kMinTilesPerSplit tiles per split: a short context runs in
+  // fewer splits (one split writes the output directly, no partials and no
+  // combine); splits past the active ones exit before touching anything
+  int tps = (ntot + NS - 1) / NS;
+  tps = tps < kMinTilesPerSplit ? kMinTilesPerSplit : tps;
+  const int nsp = (ntot + tps - 1) / tps;       // active splits
+  if (split >= nsp) return;
+  const int tb = split * tps, te = min(ntot, tb + tps);
   (void)nslots;
   // K / V chunks of a tile in registers; tile ti+1 is fetched while tile ti
   // is computed (one memory latency per split instead of one per tile)
@@ -460,7 +467,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
       o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[j], 0, 0, 0);
     }
   }
-  if (NS == 1) {
+  if (nsp == 1) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int hrow = 4 * (lane >> 4) + r;
@@ -504,8 +511,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
       ticket = __hip_atomic_fetch_add(&a.sems[b], 1, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if (ticket != NS - 1) return;
-    const int nsp = (ntot + tps - 1) / tps;     // splits that held tiles
+    if (ticket != nsp - 1) return;
     const float* pb = a.parts + (int64_t)b * NS * PS;
     // every load of the combine is issued before the first use (fixed trip
     // counts, splits >= nsp predicated off): one memory round trip instead

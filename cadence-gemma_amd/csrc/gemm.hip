@@ -1234,10 +1234,22 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(
   const int m = blockIdx.x;
   float v = -INFINITY;
   int idx = 0x7fffffff;
-  for (int i = threadIdx.x; i < nblk; i += 256) {
-    const float ov = bval[(int64_t)m * nblk + i];
-    const int oi = bidx[(int64_t)m * nblk + i];
-    if (argmax_better(ov, oi, v, idx)) { v = ov; idx = oi; }
+  // 16 (value, index) pairs per thread per pass, every load issued before
+  // the first compare; indices past nblk re-read the last pair (a duplicate
+  // never changes the argmax)
+  constexpr int PER = 16;
+  for (int base = 0; base < nblk; base += 256 * PER) {
+    float ov[PER];
+    int oi[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int64_t i = (int64_t)m * nblk + min(base + u * 256 + (int)threadIdx.x, nblk - 1);
+      ov[u] = bval[i];
+      oi[u] = bidx[i];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u)
+      if (argmax_better(ov[u], oi[u], v, idx)) { v = ov[u]; idx = oi[u]; }
   }
   for (int off = 32; off > 0; off >>= 1) {
     const float ov = __shfl_xor(v, off, 64);
