@@ -1420,14 +1420,24 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
     if (ksw == 1) CADENCE_STREAM(16, 1, 1);
     else if (ksw == 2) CADENCE_STREAM(16, 2, 1);
     else if (ksw == 4) CADENCE_STREAM(16, 4, 1);
-    else if (ksw == 5) { if constexpr (std::is_same_v<Epi, EpiLinear>) CADENCE_STREAM(16, 5, 2); }
+    else if (ksw == 5) {
+      if constexpr (std::is_same_v<Epi, EpiLinear>) {
+        if (ntw == 2) CADENCE_STREAM(16, 5, 2);
+        else CADENCE_STREAM(16, 5, 1);   // N too narrow for 2 tiles per block
+      }
+    }
     else if (ntw == 2) { if constexpr (!Epi::kPaired) CADENCE_STREAM(16, 10, 2); }
     else CADENCE_STREAM(16, 10, 1);
   } else {
     if (ksw == 1) CADENCE_STREAM(32, 1, 1);
     else if (ksw == 2) CADENCE_STREAM(32, 2, 1);
     else if (ksw == 4) CADENCE_STREAM(32, 4, 1);
-    else if (ksw == 5) { if constexpr (std::is_same_v<Epi, EpiLinear>) CADENCE_STREAM(32, 5, 2); }
+    else if (ksw == 5) {
+      if constexpr (std::is_same_v<Epi, EpiLinear>) {
+        if (ntw == 2) CADENCE_STREAM(32, 5, 2);
+        else CADENCE_STREAM(32, 5, 1);   // N too narrow for 2 tiles per block
+      }
+    }
     else if (ntw == 2) { if constexpr (!Epi::kPaired) CADENCE_STREAM(32, 10, 2); }
     else CADENCE_STREAM(32, 10, 1);
   }

@@ -276,10 +276,13 @@ def test_rglru_step_matches_gates_then_scan(dev, packed):
 
 
 @pytest.mark.parametrize("m,n,k", [(32, 2560, 2560), (32, 2560, 7680),
+                                   (16, 2560, 7680), (5, 2560, 2560),
+                                   (24, 1024, 2560), (8, 4096, 10240),
                                    (7, 512, 256), (100, 512, 256)])
 def test_gemm_linear_rmsnorm(dev, m, n, k):
   """Residual GEMM fused with the following RMSNorm (decode: split-K finished
-  by the row-owned reduce+norm kernel) vs linear then rmsnorm."""
+  by the row-owned reduce+norm kernel; M <= 16, N too narrow for two column
+  tiles per block, 4 splits) vs linear then rmsnorm."""
   g = torch.Generator().manual_seed(14)
   a = rnd(m, k, gen=g).to(dev)
   w = rnd(n, k, scale=1 / math.sqrt(k), gen=g).to(dev)
