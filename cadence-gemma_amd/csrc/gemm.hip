@@ -599,14 +599,22 @@ CADENCE_DEV void big_epilogue(const Epi& epi, f32x4 (&acc)[MR][4], u16* st, int 
       else
         bcol[j] = epi.bias_at(false, min(nbase + j * 16 + csub, N - 1), g);
     }
+    // stage() returns bf16-rounded values: their bits are the top half of
+    // the fp32 word (no third conversion), and the swizzled column of
+    // (j, r) does not depend on i (rows i * 16 + ... keep row & 7)
+    int soff[NR][4];
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) soff[j][r] = sidx(rsub + r, j * 16 + csub);
 #pragma unroll
     for (int i = 0; i < MR; ++i)
 #pragma unroll
       for (int j = 0; j < NR; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          st[sidx(i * 16 + rsub + r, j * 16 + csub)] =
-              f2bf(epi.stage(acc[i][j][r], bcol[j]));
+          st[i * 16 * 64 + soff[j][r]] =
+              (u16)(__float_as_uint(epi.stage(acc[i][j][r], bcol[j])) >> 16);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     constexpr int RPI = 64 / CPRW;                 // rows per iteration
