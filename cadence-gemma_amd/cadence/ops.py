@@ -158,19 +158,22 @@ def _big_key(epi: str, M: int, N: int, K: int, groups: int = 1) -> str:
   return f"gemm_big_kernel<{epi}, {p8}, {rows // 32}>"
 
 
-_COUNTERS: dict[int, torch.Tensor] = {}
+_COUNTERS: dict[tuple, torch.Tensor] = {}
 
 
 def _counters(dev: torch.device, n: int):
-  """Zeroed int32 arrival counters of `dev` for the in-kernel split combines
-  (kernels leave them at zero); None while capturing before first use."""
+  """Zeroed int32 arrival counters for the in-kernel split combines (kernels
+  leave them at zero), one buffer per (device, stream): launches on one
+  stream run in order, launches on two streams may overlap and must not
+  share counters.  None while capturing before first use on that stream."""
   idx = dev.index if dev.index is not None else torch.cuda.current_device()
-  buf = _COUNTERS.get(idx)
+  key = (idx, torch.cuda.current_stream(idx).cuda_stream)
+  buf = _COUNTERS.get(key)
   if buf is None or buf.numel() < n:
     if torch.cuda.is_current_stream_capturing():
       return None
     buf = torch.zeros(max(n, 4096), dtype=torch.int32, device=dev)
-    _COUNTERS[idx] = buf
+    _COUNTERS[key] = buf
   return buf
 
 

@@ -228,10 +228,13 @@ class VisionEncoder(nn.Module):
     return self.config.n_visual_tokens
 
   def _side_stream(self, dev: torch.device) -> torch.cuda.Stream:
-    s = getattr(self, "_side", None)
-    if s is None or s.device != dev:
-      s = torch.cuda.Stream(device=dev)
-      self._side = s
+    """The SigLIP stream paired with the caller's current stream (callers on
+    two streams -- pipelined micro-batches -- each get their own)."""
+    sides = self.__dict__.setdefault("_sides", {})
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    s = sides.get(key)
+    if s is None:
+      s = sides[key] = torch.cuda.Stream(device=dev)
     return s
 
   def features_into(self, pixels: torch.Tensor, out2d: torch.Tensor):

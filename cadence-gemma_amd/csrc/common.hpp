@@ -62,8 +62,29 @@ CADENCE_DEV float softplusf_(float x) {
   // torch softplus(beta=1, threshold=20)
   return x > 20.0f ? x : log1pf(expf(x));
 }
+// Exact (erf) GELU, 0.5 x (1 + erf(x / sqrt 2)) (timm / projector
+// nn.GELU()), branch-free: 1 + erf(u) = erfc(-u) for u < 0 and 2 - erfc(u)
+// for u >= 0, erfc by the Chebyshev fit of Numerical Recipes' erfcc
+// (fractional error < 1.2e-7 on all of z >= 0, so the negative tail keeps
+// its relative accuracy) with the hardware exp / reciprocal; rounded to bf16
+// right after by every caller.  libm erff branches on |u| (both paths run
+// when a wave diverges, ~50 VALU per element) and made the fc1 GEMM
+// epilogue cost twice its MFMA time at K = 1024.
 CADENCE_DEV float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.5f * z);
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float q = t * hw_exp(p - z * z);       // erfc(z)
+  return 0.5f * x * (x >= 0.0f ? 2.0f - q : q);
 }
 // tanh-approximated GELU, 0.5 x (1 + tanh(z)) with z = sqrt(2/pi) (x +
 // 0.044715 x^3) (modules.py:293-295), evaluated as the identical x *

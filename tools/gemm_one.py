@@ -1,5 +1,5 @@
 """One prefill GEMM shape launched REPS times back to back (for rocprofv3
---pmc / --kernel-trace runs of a single kernel): EPI=linear|gated, SHAPE=MxNxK.
+--pmc / --kernel-trace runs of a single kernel): EPI=linear|gelu|gated, SHAPE=MxNxK.
 Random operands (DVFS: zero-filled data runs at a higher clock)."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -21,9 +21,10 @@ def main():
   if epi == "gated":
     bg = torch.zeros(N // 2, device=dev, dtype=BF)
     fn = lambda: ops.ops.gated_gelu(a, w, bg, bg)
-  else:
+  else:   # linear (no activation) or gelu (erf GELU epilogue, ViT fc1)
     out = torch.empty(M, N, device=dev, dtype=BF)
-    fn = lambda: ops.linear(a, w, out=out)
+    act = 1 if epi == "gelu" else 0
+    fn = lambda: ops.linear(a, w, act=act, out=out)
   fn()
   torch.cuda.synchronize()
   s, e = torch.cuda.Event(True), torch.cuda.Event(True)
