@@ -25,11 +25,16 @@ def main():
   reps = 20
   for ctx in (64, 128, 320, 1000, 2100):
     nt = torch.full((B,), ctx, dtype=torch.int32, device=dev)
-    for _ in range(2):
-      ops.ops.local_attention_decode_(q, kn, vn, ck, cv, nt, H)
+    # warm-up on the capture stream: the split combine's arrival counters
+    # are per stream and must exist before capture (as in the sampler)
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+      for _ in range(2):
+        ops.ops.local_attention_decode_(q, kn, vn, ck, cv, nt, H)
     torch.cuda.synchronize()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    with torch.cuda.graph(graph, stream=side):
       for _ in range(reps):
         ops.ops.local_attention_decode_(q, kn, vn, ck, cv, nt, H)
     best = 1e9
