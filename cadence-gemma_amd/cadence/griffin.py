@@ -133,7 +133,7 @@ class Griffin(nn.Module):
              (self.final_norm if final_norm else None))
       x, xn, new_cache[name] = block.fused(
           x, pos, b, length, None if cache is None else cache[name],
-          return_cache, inplace_state, xn, nxt)
+          return_cache, inplace_state, xn, nxt, next_lazy=i + 1 < n)
     if final_norm and xn is None:
       xn = ops.rmsnorm(x, self.final_norm.scale, self.final_norm.eps,
                        packed=True)

@@ -48,12 +48,14 @@ def gelu(x: torch.Tensor) -> torch.Tensor:
   return nn.functional.gelu(x, approximate="tanh")
 
 
-def _out_proj(x2d, lin: nn.Linear, resid2d, norm):
+def _out_proj(x2d, lin: nn.Linear, resid2d, norm, lazy=False):
   """Residual output projection, optionally fused with the RMSNorm that
-  consumes it (returns (out, norm(out) or None))."""
+  consumes it (returns (out, norm(out) or None)).  lazy: the consumer is a
+  norm-aware decode GEMV, so decode rows come back unnormalised with the
+  norm attached (ops.PackedRows.norm) and it applies the norm on load."""
   if norm is None:
     return ops.linear(x2d, lin.weight, lin.bias, resid=resid2d), None
-  return ops.linear_rmsnorm(x2d, lin.weight, lin.bias, resid2d, norm)
+  return ops.linear_rmsnorm(x2d, lin.weight, lin.bias, resid2d, norm, lazy=lazy)
 
 
 class LocalAttentionBlock(nn.Module):
@@ -112,7 +114,8 @@ class LocalAttentionBlock(nn.Module):
         lambda: self.qkv_weight()[:(self.num_heads + 2) * self.head_dim][ops.qkv_rope_permutation(
             self.num_heads, self.head_dim, self.proj_q.weight.device)].contiguous())
 
-  def fused(self, xn2d, pos, b, t, cache, return_cache, resid2d, norm=None):
+  def fused(self, xn2d, pos, b, t, cache, return_cache, resid2d, norm=None,
+            lazy=False):
     """Attention branch on normalised rows; returns (resid + out,
     norm(resid + out) or None, cache)."""
     h, hd = self.num_heads, self.head_dim
@@ -164,7 +167,7 @@ class LocalAttentionBlock(nn.Module):
           else:           # _attention_cache_from_prompt of the new rows
             ck, cv, nt = ops.ops.kv_cache_fill(k, v, pos, self.window_size)
             new_cache = AttentionBlockCache(ck, cv, nt)
-    out, hn = _out_proj(enc, self.proj_final, resid2d, norm)
+    out, hn = _out_proj(enc, self.proj_final, resid2d, norm, lazy)
     return out, hn, new_cache
 
   def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,
@@ -235,7 +238,7 @@ class RecurrentBlock(nn.Module):
         torch.cat([self.linear_y.bias, self.linear_x.bias]).contiguous()))
 
   def fused(self, xn2d, pos, b, t, cache, return_cache, resid2d,
-            inplace_state: bool = False, norm=None):
+            inplace_state: bool = False, norm=None, lazy=False):
     e = self.lru_width
     w, bias = self.yx_weight()
     if (inplace_state and return_cache and cache is not None and t == 1 and
@@ -247,7 +250,7 @@ class RecurrentBlock(nn.Module):
                               cache.conv1d_state)       # [M, 2E]: y | conv(x)
       gated = self.rg_lru.step_(yc[:, e:], pos.view(-1), cache.rg_lru_state,
                                 yc[:, :e], packed_out=True)
-      out, hn = _out_proj(gated, self.linear_out, resid2d, norm)
+      out, hn = _out_proj(gated, self.linear_out, resid2d, norm, lazy)
       return out, hn, cache
     yx = ops.linear(xn2d, w, bias)                       # [M, 2E]: y | x
     y_br, x_br = yx[:, :e], yx[:, e:]
@@ -310,11 +313,11 @@ class MLPBlock(nn.Module):
         self.final_w_init_variance_scale / self.expanded_width))
     nn.init.zeros_(self.ffw_down.bias)
 
-  def fused(self, xn2d, resid2d, norm=None):
+  def fused(self, xn2d, resid2d, norm=None, lazy=False):
     """resid + MLP(xn); with `norm` also returns norm(that) (else None)."""
     w, bg, bu = self.ffw_up.gated_packed()
     act = ops.gated_gelu(xn2d, w, bg, bu)
-    return _out_proj(act, self.ffw_down, resid2d, norm)
+    return _out_proj(act, self.ffw_down, resid2d, norm, lazy)
 
   def forward(self, x: torch.Tensor) -> torch.Tensor:
     zero = torch.zeros(_flat(x).shape, dtype=x.dtype, device=x.device)
@@ -366,25 +369,30 @@ class ResidualBlock(nn.Module):
     self.mlp_block.reset_parameters()
 
   def fused(self, x2d, pos, b, t, cache, return_cache,
-            inplace_state: bool = False, xn=None, next_norm=None):
+            inplace_state: bool = False, xn=None, next_norm=None,
+            next_lazy: bool = False):
     """One residual block on [B*T, D] rows.
 
     `xn` is temporal_pre_norm(x2d) when the previous block already produced
     it; `next_norm` is the RMSNorm that consumes this block's output (the
     next block's temporal_pre_norm or the final norm): each residual GEMM is
     fused with the norm that follows it.  Returns (out, next_norm(out) or
-    None, cache)."""
+    None, cache).  next_lazy: `next_norm` is the next block's
+    temporal_pre_norm, whose decode consumers (y|x + Conv1D, q|k|v + RoPE)
+    apply it on load; channel_pre_norm always feeds the gated MLP GEMV, so
+    it is left to that GEMV too."""
     if xn is None:
       xn = ops.rmsnorm(x2d, self.temporal_pre_norm.scale,
                        self.temporal_pre_norm.eps, packed=True)
     if self.temporal_block_type == common.TemporalBlockType.RECURRENT:
       resid, hn, new_cache = self.recurrent_block.fused(
           xn, pos, b, t, cache, return_cache, x2d, inplace_state,
-          self.channel_pre_norm)
+          self.channel_pre_norm, lazy=True)
     else:
       resid, hn, new_cache = self.attention_block.fused(
-          xn, pos, b, t, cache, return_cache, x2d, self.channel_pre_norm)
-    out, out_norm = self.mlp_block.fused(hn, resid, next_norm)
+          xn, pos, b, t, cache, return_cache, x2d, self.channel_pre_norm,
+          lazy=True)
+    out, out_norm = self.mlp_block.fused(hn, resid, next_norm, next_lazy)
     return out, out_norm, new_cache
 
   def forward(self, x: torch.Tensor, segment_pos: torch.Tensor,

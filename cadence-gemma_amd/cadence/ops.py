@@ -193,10 +193,24 @@ class PackedRows(NamedTuple):
   (include/cadence_kernels.h "Decode activation layout"): what the decode
   producers (RMSNorm, gated GELU, RG-LRU step, decode attention) emit and
   the decode GEMVs consume, so each wave's activation load is 1 KiB of
-  contiguous bytes.  `data` is a flat bf16 tensor of k * 16 * ceil(m/16)."""
+  contiguous bytes.  `data` is a flat bf16 tensor of k * 16 * ceil(m/16).
+
+  With `norm` set (a layers.RMSNorm), `data` holds the rows BEFORE that
+  norm (cadence_gemm_linear_residual_rows) and `src` the same rows
+  row-major: the norm-aware decode GEMVs (linear_conv1d_, qkv_rope_decode,
+  gated_gelu) apply it on load; any other consumer gets normalised rows
+  from `normalised()`."""
   data: torch.Tensor
   m: int
   k: int
+  norm: object = None
+  src: torch.Tensor | None = None
+
+  def normalised(self) -> "PackedRows":
+    if self.norm is None:
+      return self
+    return PackedRows(ops.rmsnorm(self.src, self.norm.scale, self.norm.eps, True),
+                      self.m, self.k)
 
   @property
   def shape(self):
@@ -239,6 +253,7 @@ def _arows(a, name: str):
   """(tensor to pass, lda, M, K) of a GEMM A operand: a row-major view or
   PackedRows (lda 0)."""
   if isinstance(a, PackedRows):
+    a = a.normalised()
     _need(a.data.dtype == _BF16 and a.data.is_contiguous(), f"{name}: packed rows")
     return a.data, 0, a.m, a.k
   lda = _mat(a, name)
@@ -274,6 +289,33 @@ def decode_weight(w: torch.Tensor):
   with torch.no_grad():
     packed = pack_decode(w.detach())
   w._cadence_decode = (key, packed)
+  return packed
+
+
+def fold_norm(w: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+  """bf16(w[..., k] * bf16(1 + scale[k])): an RMSNorm's scale folded into the
+  columns of the weight that consumes its output (cadence_kernels.h
+  "Deferred RMSNorm"); the same two roundings as torch on bf16 tensors."""
+  c = scale.detach() + 1.0
+  return w.detach() * c
+
+
+def decode_weight_norm(w: torch.Tensor, norm):
+  """The cached fragment-packed copy of fold_norm(w, norm.scale) for decode
+  GEMVs that normalise on load (rebuilt when `w` or the scale changes), or
+  None when it cannot be packed or would be built inside a graph capture."""
+  if w.dim() < 2 or w.shape[-2] % 16 or w.shape[-1] % 32 or not w.is_cuda:
+    return None
+  sc = norm.scale
+  c = getattr(w, "_cadence_decode_norm", None)
+  key = (w.data_ptr(), w._version, sc.data_ptr(), sc._version)
+  if c is not None and c[0] == key:
+    return c[1]
+  if torch.cuda.is_current_stream_capturing():
+    return None
+  with torch.no_grad():
+    packed = pack_decode(fold_norm(w, sc))
+  w._cadence_decode_norm = (key, packed)
   return packed
 
 
@@ -315,9 +357,9 @@ def _gemm_linear(a, w, bias, resid, out, act, row_div, row_mul, row_off,
 
 @_reg("gemm_linear_conv1d_(Tensor a, Tensor w, Tensor? bias, Tensor conv_w, "
       "Tensor conv_b, Tensor(a!) conv_state, bool w_packed=False, "
-      "int a_rows=-1) -> Tensor")
+      "int a_rows=-1, bool norm=False, float norm_eps=0.0) -> Tensor")
 def _gemm_linear_conv1d(a, w, bias, conv_w, conv_b, conv_state, w_packed=False,
-                        a_rows=-1):
+                        a_rows=-1, norm=False, norm_eps=0.0):
   """Decode y|x projection fused with the x branch's Conv1D step: returns
   [M, 2E] = (y, conv1d_step(x)); `conv_state` [M, TW-1, E] advances in place."""
   ldw = _wld(w, w_packed, "w")
@@ -337,7 +379,8 @@ def _gemm_linear_conv1d(a, w, bias, conv_w, conv_b, conv_state, w_packed=False,
   out = torch.empty(M, N, dtype=_BF16, device=a.device)
   _lib.check(_lib.load().cadence_gemm_linear_conv1d(
       _p(a), lda, _p(w), ldw, _p(bias), _p(out), N, M, N, K, E,
-      _p(conv_w.contiguous()), _p(conv_b.contiguous()), _p(conv_state), TW, _s(a)),
+      _p(conv_w.contiguous()), _p(conv_b.contiguous()), _p(conv_state), TW,
+      _norm_flag(norm, lda), float(norm_eps), _s(a)),
       "gemm_linear_conv1d")
   return out
 
@@ -384,11 +427,49 @@ def _gemm_linear_rmsnorm(a, w, bias, resid, scale, eps, w_packed=False,
   return out, nout
 
 
+def _norm_flag(norm: bool, lda: int) -> int:
+  """Normalise-on-load flag of a decode GEMV (needs packed rows)."""
+  _need(not norm or lda == 0, "norm on load needs packed rows")
+  return 1 if norm else 0
+
+
+@_reg("gemm_linear_residual_rows(Tensor a, Tensor w, Tensor? bias, "
+      "Tensor? resid, bool w_packed=False, int a_rows=-1) -> (Tensor, Tensor)")
+def _gemm_linear_residual_rows(a, w, bias, resid, w_packed=False, a_rows=-1):
+  """Decode (M <= 32) residual GEMM: (out = a . w^T + bias + resid, the same
+  rows as PackedRows data, unnormalised) -- the consumer applies the norm.
+  Split-K combined in-kernel (arrival counters of the current stream)."""
+  ldw = _wld(w, w_packed, "w")
+  N, K = w.shape[0], w.shape[1]
+  if a_rows >= 0:
+    lda, M = 0, a_rows
+    _need(a.numel() == K * 16 * (-(-M // 16)), "a: packed rows size")
+  else:
+    lda = _mat(a, "a")
+    M, K = a.shape
+  _need(w.shape[1] == K, f"K mismatch {K} vs {w.shape[1]}")
+  ldr = _mat(resid, "resid") if resid is not None else 0
+  if bias is not None:
+    _need(bias.numel() == N and bias.dtype == _BF16, "bias shape/dtype")
+  lib = _lib.load()
+  nws = lib.cadence_gemm_rmsnorm_workspace_bytes(M, N, K)
+  _need(nws > 0 and M <= 32, "residual rows: decode shapes only")
+  cnt = _counters(a.device, N // 16)
+  _need(cnt is not None, "residual rows: no arrival counters on this stream")
+  out = torch.empty(M, N, dtype=_BF16, device=a.device)
+  rows = packed_empty(M, N, a.device)
+  ws = torch.empty(nws, dtype=torch.uint8, device=a.device)
+  _lib.check(lib.cadence_gemm_linear_residual_rows(
+      _p(a), lda, _p(w), ldw, _p(bias), _p(resid), ldr, _p(out), N, _p(rows), M,
+      N, K, _p(ws), nws, _p(cnt), _s(a)), "gemm_linear_residual_rows")
+  return out, rows
+
+
 @_reg("gated_gelu(Tensor a, Tensor w_packed, Tensor bias_gate, "
       "Tensor bias_up, bool decode_layout=False, int a_rows=-1, "
-      "bool out_packed=False) -> Tensor")
+      "bool out_packed=False, bool norm=False, float norm_eps=0.0) -> Tensor")
 def _gated_gelu(a, w_packed, bias_gate, bias_up, decode_layout=False, a_rows=-1,
-                out_packed=False):
+                out_packed=False, norm=False, norm_eps=0.0):
   F, K = w_packed.shape[0] // 2, w_packed.shape[1]
   if a_rows >= 0:
     lda, M = 0, a_rows
@@ -403,7 +484,8 @@ def _gated_gelu(a, w_packed, bias_gate, bias_up, decode_layout=False, a_rows=-1,
   ev = TIMER.start(a) if _tile(M) else None
   _lib.check(_lib.load().cadence_gemm_gated_gelu(
       _p(a), lda, _p(w_packed), 0 if decode_layout else K, _p(bias_gate),
-      _p(bias_up), _p(out), 0 if out_packed else F, M, F, K, _p(ws), nws, _s(a)),
+      _p(bias_up), _p(out), 0 if out_packed else F, M, F, K, _p(ws), nws,
+      _norm_flag(norm, lda), float(norm_eps), _s(a)),
       "gated_gelu")
   if ev is not None:
     TIMER.stop(ev, _big_key("EpiGatedGelu", M, 2 * F, K), 4.0 * M * F * K, a)
@@ -699,10 +781,13 @@ def _rope_qkv(qkv, positions, H, hd, table=None):
 
 
 @_reg("qkv_rope_decode(Tensor a, Tensor w_perm, Tensor positions, int H, int hd, "
-      "Tensor? table, bool w_packed=False, int a_rows=-1) -> (Tensor, Tensor, Tensor)")
+      "Tensor? table, bool w_packed=False, int a_rows=-1, bool norm=False, "
+      "float norm_eps=0.0) -> (Tensor, Tensor, Tensor)")
 def _qkv_rope_decode(a, w_perm, positions, H, hd, table=None, w_packed=False,
-                     a_rows=-1):
-  """Decode q|k|v GEMV + RoPE; `w_perm` rows as qkv_rope_permutation()."""
+                     a_rows=-1, norm=False, norm_eps=0.0):
+  """Decode q|k|v GEMV + RoPE; `w_perm` rows as qkv_rope_permutation().
+  norm: `a` is unnormalised packed rows and `w_perm` carries the norm scale
+  (fold_norm); the rows' rsqrt is applied in-kernel."""
   ldw = _wld(w_perm, w_packed, "w_perm")
   N, K = w_perm.shape[0], w_perm.shape[1]
   _need(N == (H + 2) * hd, "w_perm rows")
@@ -719,7 +804,8 @@ def _qkv_rope_decode(a, w_perm, positions, H, hd, table=None, w_packed=False,
   tlen = table.shape[0] if table is not None else 0
   _lib.check(_lib.load().cadence_qkv_rope_decode(
       _p(a), lda, _p(w_perm), ldw, _p(positions.contiguous()), _p(q), _p(k), _p(v),
-      M, H, hd, K, _p(table), tlen, _s(a)), "qkv_rope_decode")
+      M, H, hd, K, _p(table), tlen, _norm_flag(norm, lda), float(norm_eps),
+      _s(a)), "qkv_rope_decode")
   return q, k, v
 
 
@@ -948,8 +1034,22 @@ ops = torch.ops.cadence
 def _a(x):
   """(tensor, a_rows) of an A operand: PackedRows -> (data, m), else (x, -1)."""
   if isinstance(x, PackedRows):
+    x = x.normalised()
     return x.data, x.m
   return x, -1
+
+
+def _an(x, w):
+  """(tensor, a_rows, weight, norm) of the A operand of a norm-aware decode
+  GEMV and the weight to stream: rows whose RMSNorm is still pending go as
+  they are with the fragment-packed, norm-folded weight (norm = the RMSNorm
+  module); otherwise (tensor, a_rows, decode_weight(w) or None, None)."""
+  if isinstance(x, PackedRows) and x.norm is not None and x.k <= 2560:
+    wf = decode_weight_norm(w, x.norm)
+    if wf is not None:
+      return x.data, x.m, wf, x.norm
+  a, ar = _a(x)
+  return a, ar, (decode_weight(w) if x.shape[0] <= 32 else None), None
 
 
 def linear(x2d, w, bias=None, act=0, resid=None, out=None,
@@ -972,33 +1072,45 @@ def linear(x2d, w, bias=None, act=0, resid=None, out=None,
 
 def qkv_rope_decode(x2d, w_perm, positions, H, hd):
   """Decode q, k, v (RoPE applied) from the permuted q|k|v weight."""
-  a, ar = _a(x2d)
-  wd = decode_weight(w_perm)
+  a, ar, wd, nm = _an(x2d, w_perm)
   table = rope_table(w_perm.device, hd)
+  ne = float(nm.eps) if nm is not None else 0.0
   if wd is not None:
-    return ops.qkv_rope_decode(a, wd, positions, H, hd, table, True, ar)
+    return ops.qkv_rope_decode(a, wd, positions, H, hd, table, True, ar,
+                               nm is not None, ne)
   return ops.qkv_rope_decode(a, w_perm, positions, H, hd, table, False, ar)
 
 
 def linear_conv1d_(x2d, w, bias, conv_w, conv_b, conv_state):
   """Decode recurrent-block input projection: (y, conv1d_step(x)) as one
   [M, 2E] tensor, the conv state advanced in place."""
-  M = x2d.shape[0]
-  a, ar = _a(x2d)
-  wd = decode_weight(w)
+  a, ar, wd, nm = _an(x2d, w)
   if wd is not None:
-    return ops.gemm_linear_conv1d_(a, wd, bias, conv_w, conv_b, conv_state, True, ar)
+    return ops.gemm_linear_conv1d_(a, wd, bias, conv_w, conv_b, conv_state, True, ar,
+                                   nm is not None,
+                                   float(nm.eps) if nm is not None else 0.0)
   return ops.gemm_linear_conv1d_(a, w, bias, conv_w, conv_b, conv_state, False, ar)
 
 
-def linear_rmsnorm(x2d, w, bias, resid, norm, packed_out=None):
+def linear_rmsnorm(x2d, w, bias, resid, norm, packed_out=None, lazy=False):
   """(x2d . w^T + bias + resid, norm(that)) for a layers.RMSNorm `norm`; the
-  norm output is PackedRows for decode rows (it only feeds GEMMs)."""
+  norm output is PackedRows for decode rows (it only feeds GEMMs).
+
+  lazy (decode rows whose consumer is a norm-aware GEMV): one launch, the
+  norm left to the consumer -- PackedRows of the unnormalised rows with
+  `norm` set (cadence_gemm_linear_residual_rows)."""
   M, N = x2d.shape[0], w.shape[0]
   if packed_out is None:
     packed_out = want_packed(M, N)
   a, ar = _a(x2d)
   wd = decode_weight(w) if M <= 32 else None
+  K = w.shape[1]
+  if (lazy and packed_out and wd is not None and resid is not None and
+      N % 64 == 0 and N <= 2560 and
+      _lib.load().cadence_gemm_rmsnorm_workspace_bytes(M, N, K) > 0 and
+      _counters(x2d.device, N // 16) is not None):
+    out, rows = ops.gemm_linear_residual_rows(a, wd, bias, resid, True, ar)
+    return out, PackedRows(rows, M, N, norm, out)
   out, nout = ops.gemm_linear_rmsnorm(a, wd if wd is not None else w, bias, resid,
                                       norm.scale, norm.eps, wd is not None, ar,
                                       packed_out)
@@ -1011,10 +1123,10 @@ def gated_gelu(x2d, w_packed, bias_gate, bias_up, packed_out=None):
   M, F = x2d.shape[0], w_packed.shape[0] // 2
   if packed_out is None:
     packed_out = want_packed(M, F)
-  a, ar = _a(x2d)
-  wd = decode_weight(w_packed) if M <= 32 else None
+  a, ar, wd, nm = _an(x2d, w_packed)
   out = ops.gated_gelu(a, wd if wd is not None else w_packed, bias_gate, bias_up,
-                       wd is not None, ar, packed_out)
+                       wd is not None, ar, packed_out, nm is not None,
+                       float(nm.eps) if nm is not None else 0.0)
   return PackedRows(out, M, F) if packed_out else out
 
 

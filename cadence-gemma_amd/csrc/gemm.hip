@@ -196,6 +196,34 @@ struct EpiLinearConv : EpiLinear {
   }
 };
 
+// Decode residual projection whose RMSNorm runs in the consuming GEMV
+// (stream engine, M <= 32, in-kernel split-K combine): out = bias + resid +
+// A.W^T as EpiLinear (act 0), written row-major and once more, unnormalised,
+// in the packed decode layout the consumer loads.  Bias and residual are
+// loaded at kernel start (kPrefetch), so the last-arriving split issues no
+// dependent load after its partial-slab loads.
+struct EpiResidRows : EpiLinear {
+  static constexpr bool kPrefetch = true;
+  u16* rows;                 // packed decode layout, mt = ceil(M / 16)
+  int mt;
+  struct Pref { u16 r, b; };
+  CADENCE_DEV Pref prefetch(int64_t m, int n) const {
+    const u16* zp = reinterpret_cast<const u16*>(kZeroPage);
+    return Pref{*(resid ? resid + m * ldr + n : zp), *(bias ? bias + n : zp)};
+  }
+  CADENCE_DEV void apply_pf(int64_t m, int n, float v, int, const Pref& p) const {
+    if (bias) v = add_rn(v, bf2f(p.b));
+    float r = rbf(v);
+    if (resid) r = badd(r, bf2f(p.r));
+    const u16 o = f2bf(r);
+    out[m * ldo + n] = o;
+    rows[xpk((int)m, n, mt)] = o;
+  }
+  CADENCE_DEV void apply(int64_t m, int n, float v, int g) const {
+    apply_pf(m, n, v, g, prefetch(m, n));
+  }
+};
+
 // Decode q|k|v projection with RoPE in the epilogue (stream engine, M <= 32).
 // The weight rows are pre-permuted so that each rotation pair (dims i and
 // i + hd/4 of the rotated half of a q or k head) sits in adjacent columns
@@ -255,6 +283,10 @@ struct EpiPrefetch<E, std::void_t<decltype(E::kPrefetch)>> {
   static constexpr bool value = E::kPrefetch;
 };
 
+// Decode GEMVs whose A operand may arrive unnormalised (the RMSNorm of the
+// producing residual projection applied on load, gemm_stream_kernel NORM).
+template <class E> struct EpiNormIn { static constexpr bool value = false; };
+
 struct EpiGatedGelu {
   static constexpr bool kPaired = true;
   static constexpr bool kStaged = true;
@@ -294,6 +326,10 @@ struct EpiGatedGelu {
     st16(out + xoff((int)m, f, ldo, mt), pack8(gv));
   }
 };
+
+template <int TW> struct EpiNormIn<EpiLinearConv<TW>> { static constexpr bool value = true; };
+template <> struct EpiNormIn<EpiRopeQKV> { static constexpr bool value = true; };
+template <> struct EpiNormIn<EpiGatedGelu> { static constexpr bool value = true; };
 
 // Tile epilogues (kTile): the big engine hands the whole wave tile
 // (acc[MR][4], rows mbase + 16 i + 4 (lane >> 4) + r, columns
@@ -906,16 +942,34 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
 // activation loads, not the weight stream, bound the NTW = 1 form on the
 // wide shapes); fragment-packed weights are read once, non-temporal.
 // parts == nullptr: fixed-order LDS reduction + fused epilogue.  Otherwise
-// raw fp32 partials go to parts[split][M][N] for splitk_reduce_kernel.
-template <int MS, int KSW, int NTW, class Epi>
+// raw fp32 partials go to parts[split][M][N]: for splitk_reduce_kernel /
+// reduce_rmsnorm_kernel, or (counters != nullptr) combined in-kernel by the
+// last K split of each column tile to arrive (write-through slabs, one
+// agent-scope ticket per workgroup: MI355X_MICROARCH "inter-workgroup
+// visibility", first protocol row), in split order -- the same sums as the
+// reduce kernels -- then the epilogue.
+//
+// NORM: A holds unnormalised packed rows x, W's columns carry the RMSNorm
+// scale (W[n][k] (1 + scale[k]) in bf16, ops.fold_norm), and the workgroup
+// covers all of K (one split).  Each row's sum of squares comes from the
+// MFMA pipe -- diag(X X^T) of the fragments already in registers, the
+// products exact in fp32 -- and rsqrt(mean + eps), rounded as layers.py:70-78
+// rounds var / var + eps / rsqrt, scales the fp32 dot products before the
+// epilogue.  (The reference rounds x rsqrt and its product with 1 + scale to
+// bf16 per element; doing that here made every workgroup re-normalise the
+// whole activation on the VALU: +7..13 us per GEMV, measured.)
+template <int MS, int KSW, int NTW, class Epi, bool NORM = false>
 __global__ __launch_bounds__(512) void gemm_stream_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
     int64_t ldw, int M, int N, int K, int klen, int64_t a_goff, int64_t w_goff,
-    float* __restrict__ parts, Epi epi, int packed) {
+    float* __restrict__ parts, Epi epi, int packed, int32_t* __restrict__ counters,
+    float neps) {
   constexpr int MR = MS / 16;
   static_assert(!Epi::kPaired || NTW == 1, "paired epilogues pair gate/up tiles");
   constexpr int NREP = Epi::kPaired ? 2 : NTW;
   __shared__ float red[8][MS * 16 * NREP];
+  __shared__ float nss[NORM ? 8 : 1][MS];
+  __shared__ int ticket;
   const int g = blockIdx.z;
   A += g * a_goff;
   W += g * w_goff;
@@ -965,6 +1019,19 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
     const int k = kbeg + (wave + 8 * u) * 32;
     const bool ok = k < kend;
 #pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int m = i * 16 + (lane & 15);
+      // packed rows (common.hpp xpk, mt == MR here) or row-major
+      const int64_t off = lda == 0 ? ((((int64_t)(k >> 5) * MR + i) * 64 + lane) << 3)
+                                   : (int64_t)m * lda + k + koff;
+      xa[u][i] = ld16((ok && (lda == 0 || m < M)) ? A + off : zpage);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < KSW; ++u) {
+    const int k = kbeg + (wave + 8 * u) * 32;
+    const bool ok = k < kend;
+#pragma unroll
     for (int j = 0; j < NREP; ++j) {
       // fragment-packed [N/16][K/32][64 lanes][8]: 1 KiB per load
       const int64_t off = packed
@@ -973,17 +1040,26 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
       wb[u][j] = ld16_nt(ok ? W + off : zpage);
     }
   }
+  if constexpr (NORM) {
+    // row sums of squares: diag of the 16 x 16 blocks X_i X_i^T; lane l
+    // holds C[4 (l / 16) + r][l % 16], a diagonal element when
+    // (l % 16) / 4 == l / 16 (row l % 16, r = l % 4)
+    f32x4 dg[MR];
 #pragma unroll
-  for (int u = 0; u < KSW; ++u) {
-    const int k = kbeg + (wave + 8 * u) * 32;
-    const bool ok = k < kend;
+    for (int i = 0; i < MR; ++i) dg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      const int m = i * 16 + (lane & 15);
-      // packed rows (common.hpp xpk, mt == MR here) or row-major
-      const int64_t off = lda == 0 ? ((((int64_t)(k >> 5) * MR + i) * 64 + lane) << 3)
-                                   : (int64_t)m * lda + k + koff;
-      xa[u][i] = ld16((ok && (lda == 0 || m < M)) ? A + off : zpage);
+    for (int u = 0; u < KSW; ++u)
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        dg[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8, xa[u][i]), __builtin_bit_cast(bf16x8, xa[u][i]),
+            dg[i], 0, 0, 0);
+    const int r4 = lane & 3;
+    if (((lane & 15) >> 2) == (lane >> 4)) {
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        nss[wave][i * 16 + (lane & 15)] =
+            r4 == 0 ? dg[i][0] : r4 == 1 ? dg[i][1] : r4 == 2 ? dg[i][2] : dg[i][3];
     }
   }
   f32x4 acc[MR][NREP];
@@ -1009,6 +1085,60 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
       for (int r = 0; r < 4; ++r)
         red[wave][((i * 16 + rsub + r) * NREP + j) * 16 + csub] = acc[i][j][r];
   __syncthreads();
+  if constexpr (!Epi::kPaired && !EpiPairLanes<Epi>::value) {
+    if (counters) {
+      // in-kernel split-K combine: thread o owns (row o / 16, column o % 16)
+      // of each of the NREP column tiles (MS * 16 <= 512 threads)
+      const int o = threadIdx.x, m = o / 16, c = o % 16;
+      const bool mine = o < MS * 16 && m < M;
+      const int64_t sstride = (int64_t)gridDim.z * M * N;
+      // (rows past M, which only load, read row M - 1: inside the slab)
+      float* slab = parts + (int64_t)g * M * N + (int64_t)min(m, M - 1) * N;
+      float v[NREP];
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        const int idx = (min(m, MS - 1) * NREP + j) * 16 + c;
+        v[j] = ((red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx])) +
+               ((red[4][idx] + red[5][idx]) + (red[6][idx] + red[7][idx]));
+        if (mine)
+          __hip_atomic_store(slab + blockIdx.y * sstride + col[j] + c, v[j],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0)
+        ticket = __hip_atomic_fetch_add(counters + g * gridDim.x + blockIdx.x, 1,
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if (ticket != (int)gridDim.y - 1) return;
+      constexpr int SMAX = 4;
+      const int S = gridDim.y;
+      float p[SMAX][NREP];
+#pragma unroll
+      for (int sp = 0; sp < SMAX; ++sp)
+#pragma unroll
+        for (int j = 0; j < NREP; ++j)
+          p[sp][j] = __hip_atomic_load(slab + min(sp, S - 1) * sstride + col[j] + c,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (mine) {
+#pragma unroll
+        for (int j = 0; j < NREP; ++j) {
+          float t = 0.0f;
+#pragma unroll
+          for (int sp = 0; sp < SMAX; ++sp)
+            if (sp < S) t += sp == (int)blockIdx.y ? v[j] : p[sp][j];
+          if constexpr (EpiPrefetch<Epi>::value)
+            epi.apply_pf(m, col[j] + c, t, g, pf[j]);
+          else
+            epi.apply(m, col[j] + c, t, g);
+        }
+      }
+      if (threadIdx.x == 0)
+        __hip_atomic_store(counters + g * gridDim.x + blockIdx.x, 0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
   for (int o = threadIdx.x; o < MS * 16; o += 512) {
     const int m = o / 16, c = o % 16;
     if (m >= M) continue;
@@ -1018,6 +1148,14 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
       const int idx = (m * NREP + j) * 16 + c;
       v[j] = ((red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx])) +
              ((red[4][idx] + red[5][idx]) + (red[6][idx] + red[7][idx]));
+    }
+    if constexpr (NORM) {
+      const float ss = ((nss[0][m] + nss[1][m]) + (nss[2][m] + nss[3][m])) +
+                       ((nss[4][m] + nss[5][m]) + (nss[6][m] + nss[7][m]));
+      const float var = rbf(ss / (float)K);
+      const float rs = rbf(1.0f / sqrtf(rbf(var + neps)));
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) v[j] *= rs;
     }
     if (parts) {
       float* dst = parts + ((int64_t)blockIdx.y * gridDim.z + g) * (int64_t)M * N +
@@ -1405,31 +1543,36 @@ int64_t skinny_klen(int64_t K, int splits) {
   return klen;
 }
 
-// Stream engine launch: `splits` K splits (raw fp32 partials to `parts`
-// [split][group][M][N] when > 1, else the epilogue runs in-kernel).
+// Column tiles per stream-engine workgroup: two when that still leaves >= 150
+// workgroups (cold-weight sweep, tools/gemv_lab.py: xy 12.7 -> 8.9 us, down
+// 18.6 -> 13).
 template <class Epi>
-void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
-                   int64_t M, int64_t N, int64_t K, int64_t groups,
-                   int64_t a_goff, int64_t w_goff, const Epi& epi, int ksw,
-                   int splits, float* parts, int packed, hipStream_t st) {
-  // two column tiles per workgroup when that still leaves >= 150 workgroups
-  // (cold-weight sweep, tools/gemv_lab.py: xy 12.7 -> 8.9 us, down 18.6 -> 13)
-  const int ntw = (!Epi::kPaired && (ksw == 10 || ksw == 5) && N % 32 == 0 &&
-                   (N / 32) * splits * groups >= 150) ? 2 : 1;
+int stream_ntw(int64_t N, int ksw, int splits, int64_t groups) {
+  return (!Epi::kPaired && (ksw == 10 || ksw == 5) && N % 32 == 0 &&
+          (N / 32) * splits * groups >= 150) ? 2 : 1;
+}
+
+template <class Epi, bool NORM>
+void launch_stream_t(const u16* A, int64_t lda, const u16* W, int64_t ldw,
+                     int64_t M, int64_t N, int64_t K, int64_t groups,
+                     int64_t a_goff, int64_t w_goff, const Epi& epi, int ksw,
+                     int splits, float* parts, int packed, hipStream_t st,
+                     int32_t* counters, float neps) {
+  const int ntw = stream_ntw<Epi>(N, ksw, splits, groups);
   const unsigned nblk = (unsigned)(Epi::kPaired ? N / 32 : N / 16 / ntw);
   const int64_t ks = K / 32;
   const int klen = (int)((ks + splits - 1) / splits) * 32;
   dim3 grid(nblk, (unsigned)splits, (unsigned)groups);
-#define CADENCE_STREAM(MS_, KSW_, NTW_)                                          \
-  hipLaunchKernelGGL((gemm_stream_kernel<MS_, KSW_, NTW_, Epi>), grid, dim3(512), \
-                     0, st, A, lda, W, ldw, (int)M, (int)N, (int)K, klen, a_goff, \
-                     w_goff, parts, epi, packed)
+#define CADENCE_STREAM(MS_, KSW_, NTW_)                                               \
+  hipLaunchKernelGGL((gemm_stream_kernel<MS_, KSW_, NTW_, Epi, NORM>), grid, dim3(512), \
+                     0, st, A, lda, W, ldw, (int)M, (int)N, (int)K, klen, a_goff,      \
+                     w_goff, parts, epi, packed, counters, neps)
   if (M <= 16) {
     if (ksw == 1) CADENCE_STREAM(16, 1, 1);
     else if (ksw == 2) CADENCE_STREAM(16, 2, 1);
     else if (ksw == 4) CADENCE_STREAM(16, 4, 1);
     else if (ksw == 5) {
-      if constexpr (std::is_same_v<Epi, EpiLinear>) {
+      if constexpr (std::is_same_v<Epi, EpiLinear> || std::is_same_v<Epi, EpiResidRows>) {
         if (ntw == 2) CADENCE_STREAM(16, 5, 2);
         else CADENCE_STREAM(16, 5, 1);   // N too narrow for 2 tiles per block
       }
@@ -1441,7 +1584,7 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
     else if (ksw == 2) CADENCE_STREAM(32, 2, 1);
     else if (ksw == 4) CADENCE_STREAM(32, 4, 1);
     else if (ksw == 5) {
-      if constexpr (std::is_same_v<Epi, EpiLinear>) {
+      if constexpr (std::is_same_v<Epi, EpiLinear> || std::is_same_v<Epi, EpiResidRows>) {
         if (ntw == 2) CADENCE_STREAM(32, 5, 2);
         else CADENCE_STREAM(32, 5, 1);   // N too narrow for 2 tiles per block
       }
@@ -1450,6 +1593,29 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
     else CADENCE_STREAM(32, 10, 1);
   }
 #undef CADENCE_STREAM
+}
+
+// Stream engine launch: `splits` K splits (raw fp32 partials to `parts`
+// [split][group][M][N] when > 1: reduced by a second kernel, or in-kernel
+// when `counters` is given, else the epilogue runs in-kernel).  `norm`: A is
+// unnormalised packed rows and W carries the norm scale; the rows' rsqrt is
+// applied in-kernel (gemm_stream_kernel NORM; one split only).
+template <class Epi>
+void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
+                   int64_t M, int64_t N, int64_t K, int64_t groups,
+                   int64_t a_goff, int64_t w_goff, const Epi& epi, int ksw,
+                   int splits, float* parts, int packed, hipStream_t st,
+                   int32_t* counters = nullptr, int norm = 0,
+                   float neps = 0.0f) {
+  if constexpr (EpiNormIn<Epi>::value) {
+    if (norm) {
+      launch_stream_t<Epi, true>(A, lda, W, ldw, M, N, K, groups, a_goff, w_goff, epi,
+                                 ksw, splits, parts, packed, st, counters, neps);
+      return;
+    }
+  }
+  launch_stream_t<Epi, false>(A, lda, W, ldw, M, N, K, groups, a_goff, w_goff, epi, ksw,
+                              splits, parts, packed, st, counters, 0.0f);
 }
 
 // Prefill engine plan for M > kSkinnyMaxM: 0 = 2-buffer 256-row kernel,
@@ -1483,8 +1649,14 @@ template <class Epi>
 int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                 int64_t N, int64_t K, int64_t groups, int64_t a_goff,
                 int64_t w_goff, const Epi& epi, void* ws, int64_t ws_bytes,
-                hipStream_t st) {
+                hipStream_t st, int norm = 0, float neps = 0.0f) {
   if (M <= 0) return 0;
+  // norm (normalise-on-load) needs packed rows and one weight-stream split
+  if (norm) {
+    int ksw = 0, ss = 0;
+    if (lda != 0 || !stream_plan(M, K, &ksw, &ss) || ss != 1)
+      return (int)hipErrorInvalidValue;
+  }
   // ldw == 0: W is fragment-packed (see cadence_kernels.h), decode engines only
   const int packed = ldw == 0 ? 1 : 0;
   if (packed && (M > kSkinnyMaxM || N % 16 || K % 32)) return (int)hipErrorInvalidValue;
@@ -1538,7 +1710,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
       parts = static_cast<float*>(ws);
     }
     launch_stream(A, lda, W, ldw, M, N, K, groups, a_goff, w_goff, epi, ksw,
-                  ssplits, parts, packed, st);
+                  ssplits, parts, packed, st, nullptr, norm, neps);
     if (ssplits > 1) {
       int64_t outs = M * N;
       int rblocks = (int)((outs + 255) / 256);
@@ -1579,7 +1751,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 10; }
+int cadence_abi_version(void) { return 11; }
 
 int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
   if (M <= kSkinnyMaxM || M <= 0) return 0;
@@ -1617,9 +1789,11 @@ int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
                                int64_t ldo, int64_t M, int64_t N, int64_t K,
                                int64_t conv_lo, const void* conv_w,
                                const void* conv_b, void* conv_state,
-                               int64_t temporal_width, void* stream) {
+                               int64_t temporal_width, int norm,
+                               float norm_eps, void* stream) {
   if (M <= 0) return 0;
   const int64_t E = N - conv_lo;
+  if (norm && lda != 0) return (int)hipErrorInvalidValue;
   int ksw = 0, ss = 0;
   if (M > 32 || N % 64 || K % 32 || ldo < N || conv_lo < 0 || E <= 0 ||
       temporal_width < 1 || temporal_width > 4 || !conv_w || !conv_b ||
@@ -1639,7 +1813,7 @@ int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
     epi.E = (int)E;
     launch_stream(static_cast<const u16*>(A), lda, static_cast<const u16*>(W), ldw, M,
                   N, K, 1, 0, 0, epi, ksw, 1, nullptr, ldw == 0 ? 1 : 0,
-                  static_cast<hipStream_t>(stream));
+                  static_cast<hipStream_t>(stream), nullptr, norm, norm_eps);
   };
   switch (temporal_width) {   // Griffin uses 4; 1-3 for API parity
     case 1: run(std::integral_constant<int, 1>{}); break;
@@ -1654,8 +1828,10 @@ int cadence_qkv_rope_decode(const void* A, int64_t lda, const void* Wperm,
                             int64_t ldw, const int32_t* positions, void* q_out,
                             void* k_out, void* v_out, int64_t M, int64_t H,
                             int64_t hd, int64_t K, const void* table,
-                            int64_t table_len, void* stream) {
+                            int64_t table_len, int norm,
+                            float norm_eps, void* stream) {
   if (M <= 0) return 0;
+  if (norm && lda != 0) return (int)hipErrorInvalidValue;
   const int64_t N = (H + 2) * hd;
   int ksw = 0, ss = 0;
   if (M > 32 || hd % 64 || H < 1 || K % 32 || (ldw != 0 && ldw < K) ||
@@ -1666,7 +1842,7 @@ int cadence_qkv_rope_decode(const void* A, int64_t lda, const void* Wperm,
                  table ? (int)table_len : 0, (int)H, (int)hd};
   launch_stream(static_cast<const u16*>(A), lda, static_cast<const u16*>(Wperm), ldw,
                 M, N, K, 1, 0, 0, epi, ksw, 1, nullptr, ldw == 0 ? 1 : 0,
-                static_cast<hipStream_t>(stream));
+                static_cast<hipStream_t>(stream), nullptr, norm, norm_eps);
   return (int)hipGetLastError();
 }
 
@@ -1725,11 +1901,38 @@ int cadence_gemm_linear_rmsnorm(const void* A, int64_t lda, const void* W,
   return cadence_rmsnorm(out, ldo, norm_scale, norm_out, ld_norm, M, N, eps, stream);
 }
 
+int cadence_gemm_linear_residual_rows(const void* A, int64_t lda, const void* W,
+                                      int64_t ldw, const void* bias,
+                                      const void* resid, int64_t ld_resid,
+                                      void* out, int64_t ldo, void* out_rows,
+                                      int64_t M, int64_t N, int64_t K,
+                                      void* workspace, int64_t ws_bytes,
+                                      int32_t* counters, void* stream) {
+  if (M <= 0) return 0;
+  int ksw = 0, ss = 0;
+  if (M > 32 || N % 64 || N > 4096 || ldo < N || (resid && ld_resid < N) ||
+      !out_rows || !counters || (ldw != 0 && ldw < K) || (lda != 0 && lda < K) ||
+      !rmsnorm_stream_plan(M, K, &ksw, &ss))
+    return (int)hipErrorInvalidValue;
+  if (!workspace || ws_bytes < (int64_t)ss * M * N * 4) return (int)hipErrorInvalidValue;
+  EpiResidRows epi{};
+  static_cast<EpiLinear&>(epi) =
+      EpiLinear{static_cast<u16*>(out), ldo, static_cast<const u16*>(bias),
+                static_cast<const u16*>(resid), ld_resid, 0, RowMap{M, 0, 0}, 0.0f};
+  epi.rows = static_cast<u16*>(out_rows);
+  epi.mt = (int)((M + 15) / 16);
+  launch_stream(static_cast<const u16*>(A), lda, static_cast<const u16*>(W), ldw, M, N,
+                K, 1, 0, 0, epi, ksw, ss, static_cast<float*>(workspace),
+                ldw == 0 ? 1 : 0, static_cast<hipStream_t>(stream), counters);
+  return (int)hipGetLastError();
+}
+
 int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
                             int64_t ldw, const void* bias_gate,
                             const void* bias_up, void* out, int64_t ldo,
                             int64_t M, int64_t F, int64_t K, void* workspace,
-                            int64_t ws_bytes, void* stream) {
+                            int64_t ws_bytes, int norm,
+                            float norm_eps, void* stream) {
   if (F % 64 || (ldw != 0 && ldw < K)) return (int)hipErrorInvalidValue;
   if (ldo == 0 && M > 32) return (int)hipErrorInvalidValue;   // packed rows
   EpiGatedGelu epi{static_cast<u16*>(out), ldo,
@@ -1737,7 +1940,8 @@ int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
                    static_cast<const u16*>(bias_up), (int)((M + 15) / 16)};
   return launch_gemm(static_cast<const u16*>(A), lda,
                      static_cast<const u16*>(Wpacked), ldw, M, 2 * F, K, 1, 0, 0,
-                     epi, workspace, ws_bytes, static_cast<hipStream_t>(stream));
+                     epi, workspace, ws_bytes, static_cast<hipStream_t>(stream),
+                     norm, norm_eps);
 }
 
 int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,

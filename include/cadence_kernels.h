@@ -33,10 +33,23 @@
  * instruction (row-major fragment loads halve its weight-stream rate).
  * Requires K % 32 == 0; a packed buffer holds K * 16 * mt elements.
  * Producers: cadence_rmsnorm (ldo = 0), cadence_gemm_linear_rmsnorm
- * (ld_norm = 0), cadence_gemm_gated_gelu (ldo = 0), cadence_rglru_step
+ * (ld_norm = 0), cadence_gemm_linear_residual_rows (out_rows, unnormalised),
+ * cadence_gemm_gated_gelu (ldo = 0), cadence_rglru_step
  * (ldy = 0), cadence_local_attention_decode (ld_out = 0).  Consumers: the
  * A operand of cadence_gemm_linear, cadence_gemm_linear_rmsnorm,
  * cadence_gemm_gated_gelu, cadence_gemm_logits, cadence_logits_argmax.
+ *
+ * Deferred RMSNorm (decode): a residual projection that feeds an RMSNorm
+ * (y = RMSNorm(x) = bf16(bf16(x * r) * (1 + s)), r = rsqrt(mean(x^2) + eps),
+ * layers.py:70-78) may hand the consuming GEMV the unnormalised rows x
+ * (cadence_gemm_linear_residual_rows).  The consumer's W then holds
+ * bf16(W[n][k] * bf16(1 + s[k])) (the scale folded into the weight columns,
+ * once per weight), and the kernel computes each row's r from x (sum of
+ * squares in fp32 on the MFMA pipe; var, var + eps and r rounded to bf16 as
+ * the reference) and scales the fp32 dot products by r before its
+ * epilogue.  Equal to the reference up to the per-element bf16 roundings of
+ * x * r and of the product with 1 + s, which it skips (tolerance-tested,
+ * tests/test_decode_norm_gpu.py).
  *
  * The reference (`surakku/cadence-gemma`) has no native layer: each entry
  * point replaces a sequence of eager PyTorch ops (or timm ops) of the
@@ -93,13 +106,17 @@ int cadence_gemm_linear(const void* A, int64_t lda, const void* W, int64_t ldw,
  *   out[:, conv_lo:]  = conv1d_step(yx[:, conv_lo:]; conv_w [TW][E], conv_b,
  *                                   conv_state [M][TW-1][E], shifted in place)
  * W may be fragment-packed (ldw == 0) and A packed rows (lda == 0).  K must
- * fit one split of the weight-streaming engine (K <= 2560); TW <= 4. */
+ * fit one split of the weight-streaming engine (K <= 2560); TW <= 4.
+ * norm != 0: normalise on load (see "Deferred RMSNorm" above): A is the
+ * unnormalised packed rows of cadence_gemm_linear_residual_rows and W carries
+ * the block's temporal_pre_norm scale. */
 int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
                                int64_t ldw, const void* bias, void* out,
                                int64_t ldo, int64_t M, int64_t N, int64_t K,
                                int64_t conv_lo, const void* conv_w,
                                const void* conv_b, void* conv_state,
-                               int64_t temporal_width, void* stream);
+                               int64_t temporal_width, int norm,
+                               float norm_eps, void* stream);
 
 /* Residual GEMM that feeds an RMSNorm (the temporal-block output projection
  * and ffw_down, each followed by the next norm; modules.py:908-913):
@@ -118,16 +135,39 @@ int cadence_gemm_linear_rmsnorm(const void* A, int64_t lda, const void* W,
                                 void* workspace, int64_t ws_bytes,
                                 void* stream);
 
+/* Decode form of the residual GEMM above whose RMSNorm is deferred to the
+ * GEMM that consumes it (M <= 32 sequences; same K split plan and workspace
+ * as cadence_gemm_linear_rmsnorm):
+ *   out      = A . W^T + bias + resid      (row-major, ldo)
+ *   out_rows = the same values in the packed decode layout, NOT normalised
+ * The K splits of each column tile are combined inside the launch by the
+ * last split to arrive, in split order (the sums of the two-kernel form).
+ * Consumers normalise on load (norm != 0): cadence_gemm_linear_conv1d,
+ * cadence_qkv_rope_decode, cadence_gemm_gated_gelu.  counters: >= N / 16 zeroed int32, left zeroed
+ * (launches that may overlap need their own).  Replaces the same reference
+ * lines as cadence_gemm_linear_rmsnorm (modules.py:908-913 + the next
+ * norm). */
+int cadence_gemm_linear_residual_rows(const void* A, int64_t lda, const void* W,
+                                      int64_t ldw, const void* bias,
+                                      const void* resid, int64_t ld_resid,
+                                      void* out, int64_t ldo, void* out_rows,
+                                      int64_t M, int64_t N, int64_t K,
+                                      void* workspace, int64_t ws_bytes,
+                                      int32_t* counters, void* stream);
+
 /* MLP up-projection + gating: out[m, f] = gelu_tanh(x.Wg[f] + bg[f]) *
  * (x.Wu[f] + bu[f]).  W is the packed [2F][K] matrix in which every 64-row
  * group g holds 32 gate rows then the 32 up rows of features
  * [32g, 32g + 32).  Replaces modules.py:754-756 (Einsum ffw_up + gelu + mul;
- * layers.py:726-729). */
+ * layers.py:726-729).  norm != 0 (M <= 32, packed rows, K <= 2560):
+ * normalise on load ("Deferred RMSNorm" above; W carries channel_pre_norm's
+ * scale). */
 int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
                             int64_t ldw, const void* bias_gate,
                             const void* bias_up, void* out, int64_t ldo,
                             int64_t M, int64_t F, int64_t K, void* workspace,
-                            int64_t ws_bytes, void* stream);
+                            int64_t ws_bytes, int norm, float norm_eps,
+                            void* stream);
 
 /* RG-LRU gates: both BlockDiagonalLinear layers of one RG-LRU as a grouped
  * GEMM (one group per head, K = block width) with the full gate chain fused
@@ -274,12 +314,14 @@ int cadence_rope_qkv(const void* qkv, int64_t ldqkv, const int32_t* positions,
  * for i < hd/4 (the rotated half's pairs side by side; rows hd/2.. and the
  * v head in natural order).  Outputs q [M][H*hd], k [M][hd], v [M][hd] as
  * cadence_rope_qkv writes them.  Wperm may be fragment-packed (ldw == 0), A
- * packed rows (lda == 0); K <= 2560 (one split). */
+ * packed rows (lda == 0); K <= 2560 (one split).  norm != 0: normalise on
+ * load ("Deferred RMSNorm" above; W carries temporal_pre_norm's scale). */
 int cadence_qkv_rope_decode(const void* A, int64_t lda, const void* Wperm,
                             int64_t ldw, const int32_t* positions, void* q_out,
                             void* k_out, void* v_out, int64_t M, int64_t H,
                             int64_t hd, int64_t K, const void* table,
-                            int64_t table_len, void* stream);
+                            int64_t table_len, int norm, float norm_eps,
+                            void* stream);
 
 /* sin / cos table for cadence_rope_qkv: table[p][0][i] = bf16(sin(p * f_i)),
  * table[p][1][i] = bf16(cos(p * f_i)), i < hd / 4, f_i as modules.py:73-77
