@@ -501,7 +501,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
       for (int q = tid * 4; q < PS; q += 1024) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(q < 32 ? ml + q : stage + (q - 32));
         float* dst = part + q;
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(dst), "v"(v) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(dst), "v"(v) : "memory");
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -49,16 +49,14 @@ constexpr int GA_KT = 64;      // keys per tile
 constexpr int GA_QB = 16;      // queries per workgroup
 constexpr int GA_MAXW = 10;    // waves (= heads) per workgroup, at most
 
+// Compiler-visible maxes (not inline asm): the hazard recognizer must see
+// these reads of fresh MFMA results and the permlane reads of their outputs
+// (an asm VALU reading an MFMA's D within ~12 wait states reads stale
+// accumulators -- seen as run-to-run output differences in the ViT kernel).
 CADENCE_DEV float ga_max3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return __builtin_fmaxf(__builtin_fmaxf(a, b), c);
 }
-CADENCE_DEV float ga_max2(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
+CADENCE_DEV float ga_max2(float a, float b) { return __builtin_fmaxf(a, b); }
 // max over lanes l, l ^ 16, l ^ 32, l ^ 48 (the four key groups of a query)
 CADENCE_DEV float ga_max_rows(float v) {
   const uint32_t u = __float_as_uint(v);

@@ -26,18 +26,14 @@ namespace {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-// max without the IEEE sNaN-quieting v_max the fmaxf lowering adds (scores
-// are finite or -inf)
+// max of scores that are finite or -inf.  Compiler-visible (not inline
+// asm): the hazard recognizer must see these reads of fresh MFMA results
+// (an MFMA's D read by an asm VALU within ~12 wait states reads stale
+// accumulators -- observed as run-to-run differences in the output).
 CADENCE_DEV float max3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return __builtin_fmaxf(__builtin_fmaxf(a, b), c);
 }
-CADENCE_DEV float max2(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
+CADENCE_DEV float max2(float a, float b) { return __builtin_fmaxf(a, b); }
 // max over lanes l, l ^ 16, l ^ 32, l ^ 48 (the four 16-lane rows) with the
 // gfx950 row swaps instead of two LDS-routed ds_bpermute
 CADENCE_DEV float max_rows(float v) {
@@ -79,7 +75,7 @@ CADENCE_DEV int kswz(int ch, int row) {
 // zero) and VR = hd rows of V^T (O^T rows >= hd read row VR - 1 and are
 // discarded) -- for hd 72 that is 79 KB, two workgroups per CU.
 template <int HDK, int HDV, int NPMAX, int NW, int QT, int KW = HDK / 8, int VR = HDV>
-__global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
+__global__ __launch_bounds__(NW * 64, 4) void vit_attn_kernel(
     const u16* __restrict__ qkv, u16* __restrict__ out, int N, int H, int hd,
     float scale_log2) {
   constexpr int CPR = KW;             // stored 16-B chunks per K row
@@ -117,37 +113,6 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
   const int np = (N + 31) & ~31;
   const uint4 zero = make_uint4(0, 0, 0, 0);
 
-  // K -> LDS, zero-filled past N and past hd
-  for (int c = tid; c < np * CPR; c += NW * 64) {
-    const int key = c / CPR, ch = c % CPR;
-    uint4 v = zero;
-    if (key < N && ch * 8 < hd) v = ld16(kb + key * rs + ch * 8);
-    kimg[key * CPR + kswz<CPR>(ch, key)] = v;
-  }
-  // V^T -> LDS: one item = 4 keys x 8 dims, written as 8 runs of 4 keys
-  for (int it = tid; it < (np / 4) * VCH; it += NW * 64) {
-    const int kq = it / VCH, dc = it % VCH;
-    uint4 v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int key = kq * 4 + j;
-      v[j] = (key < N && dc * 8 < hd) ? ld16(vb + key * rs + dc * 8) : zero;
-    }
-    const uint32_t w[4][4] = {{v[0].x, v[0].y, v[0].z, v[0].w},
-                              {v[1].x, v[1].y, v[1].z, v[1].w},
-                              {v[2].x, v[2].y, v[2].z, v[2].w},
-                              {v[3].x, v[3].y, v[3].z, v[3].w}};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int sh = (i & 1) * 16;
-      const uint32_t e0 = (w[0][i >> 1] >> sh) & 0xffffu, e1 = (w[1][i >> 1] >> sh) & 0xffffu;
-      const uint32_t e2 = (w[2][i >> 1] >> sh) & 0xffffu, e3 = (w[3][i >> 1] >> sh) & 0xffffu;
-      *reinterpret_cast<uint2*>(&vt[(dc * 8 + i) * VTS + vslot(kq * 4)]) =
-          make_uint2(e0 | (e1 << 16), e2 | (e3 << 16));
-    }
-  }
-  __syncthreads();
-
   const int g = lane >> 4, c16 = lane & 15;
   const int nqt = (N + 15) >> 4;
   // QT query tiles per pass share every K / V^T fragment read and give the
@@ -164,8 +129,65 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(
         dst[u][ks] = ld16(qb + qq * rs + min(ks * 32 + 8 * g, hd - 8));
     }
   };
+  // K -> LDS (zero-filled past N and past hd) and V^T -> LDS (one item = 4
+  // keys x 8 dims, written as 8 runs of 4 keys).  Every staging load of the
+  // thread is issued before the first LDS write (branch-free: absent chunks
+  // read the zero page), and the first Q fragments with them: one memory
+  // round trip for the whole staging instead of one per loop iteration.
+  constexpr int NT = NW * 64;
+  constexpr int KIT = (NPMAX * CPR + NT - 1) / NT;
+  constexpr int VIT = ((NPMAX / 4) * VCH + NT - 1) / NT;
+  const u16* zpage = reinterpret_cast<const u16*>(kZeroPage + lane);
+  uint4 kv[KIT], vv[VIT][4];
+#pragma unroll
+  for (int i = 0; i < KIT; ++i) {
+    const int c = tid + i * NT;
+    const int key = c / CPR, ch = c % CPR;
+    const bool ok = c < np * CPR && key < N && ch * 8 < hd;
+    kv[i] = ld16(ok ? kb + key * rs + ch * 8 : zpage);
+  }
+#pragma unroll
+  for (int i = 0; i < VIT; ++i) {
+    const int it = tid + i * NT;
+    const int kq = it / VCH, dc = it % VCH;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int key = kq * 4 + j;
+      const bool ok = it < (np / 4) * VCH && key < N && dc * 8 < hd;
+      vv[i][j] = ld16(ok ? vb + key * rs + dc * 8 : zpage);
+    }
+  }
   uint4 qn[QT][KS];
   load_q(wave * QT, qn);
+#pragma unroll
+  for (int i = 0; i < KIT; ++i) {
+    const int c = tid + i * NT;
+    if (c < np * CPR) {
+      const int key = c / CPR, ch = c % CPR;
+      kimg[key * CPR + kswz<CPR>(ch, key)] = kv[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VIT; ++i) {
+    const int it = tid + i * NT;
+    if (it < (np / 4) * VCH) {
+      const int kq = it / VCH, dc = it % VCH;
+      const uint32_t w[4][4] = {{vv[i][0].x, vv[i][0].y, vv[i][0].z, vv[i][0].w},
+                                {vv[i][1].x, vv[i][1].y, vv[i][1].z, vv[i][1].w},
+                                {vv[i][2].x, vv[i][2].y, vv[i][2].z, vv[i][2].w},
+                                {vv[i][3].x, vv[i][3].y, vv[i][3].z, vv[i][3].w}};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int sh = (e & 1) * 16;
+        const uint32_t e0 = (w[0][e >> 1] >> sh) & 0xffffu, e1 = (w[1][e >> 1] >> sh) & 0xffffu;
+        const uint32_t e2 = (w[2][e >> 1] >> sh) & 0xffffu, e3 = (w[3][e >> 1] >> sh) & 0xffffu;
+        *reinterpret_cast<uint2*>(&vt[(dc * 8 + e) * VTS + vslot(kq * 4)]) =
+            make_uint2(e0 | (e1 << 16), e2 | (e3 << 16));
+      }
+    }
+  }
+  __syncthreads();
+
   for (int qt0 = wave * QT; qt0 < nqt; qt0 += NW * QT) {
     int q[QT];
     bf16x8 qf[QT][KS];
