@@ -1619,13 +1619,18 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
 }
 
 // Prefill engine plan for M > kSkinnyMaxM: 0 = 2-buffer 256-row kernel,
-// 256 / 224 = 8-phase kernel with that tile height.
+// 160 / 192 / 224 / 256 = 8-phase kernel with that tile height.
 //  * 8-phase when K splits into pairs of 64-deep tiles (an A/B of the
 //    guide's two-barrier phase -- reads, barrier, lgkmcnt(0), MFMAs,
 //    barrier -- ran 1-5 % slower on every prefill shape);
 //  * tile height 256 or 224 rows, whichever needs fewer (rounds x rows) on
 //    the CUs (M = 10208 = 32 x 319: 460 tiles of 224 in 2 rounds beat 400 of
-//    256 in 2 rounds).
+//    256 in 2 rounds);
+//  * 192 or 160 rows where that saves > 5 % of rounds x (MR + 2), MR =
+//    rows / 32 (a tile's time: its MR MFMA row blocks plus ~2 blocks' worth
+//    of fixed prologue / DMA / epilogue) -- the narrow ViT GEMMs (N = 1024 /
+//    1152: 4-5 column panels, 152-185 tiles of 224 rows for 256 CUs) and the
+//    ViT MLP up-projections (608 tiles: 3 rounds of 224, or 3 of 192).
 int big_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -1637,12 +1642,20 @@ int big_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
   }();
   if (K % (2 * BK) != 0) return 0;
   const int64_t ntn = (N + 255) / 256;
-  auto rounds_x_rows = [&](int64_t bm) {
+  auto rounds = [&](int64_t bm) {
     const int64_t t = ((M + bm - 1) / bm) * ntn * groups;
-    return ((t + cus - 1) / cus) * bm;
+    return (t + cus - 1) / cus;
   };
-  if (rounds_x_rows(224) < rounds_x_rows(256)) return 224;
-  return 256;
+  int best = rounds(224) * 224 < rounds(256) * 256 ? 224 : 256;
+  double cost = (double)rounds(best) * (best / 32 + 2);
+  for (int mr = 6; mr >= 5; --mr) {
+    const double c = (double)rounds(32 * mr) * (mr + 2);
+    if (c < 0.95 * cost) {
+      best = 32 * mr;
+      cost = c;
+    }
+  }
+  return best;
 }
 
 template <class Epi>
@@ -1665,13 +1678,18 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
     if (N % 64 || K % BK) return (int)hipErrorInvalidValue;
     const int rows = big_tile_rows(M, N, K, groups);
     const bool p8 = rows != 0;
-    const bool bm224 = rows == 224;
-    const int64_t bm = bm224 ? 224 : 256;
+    const int64_t bm = p8 ? rows : 256;
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + 255) / 256);
     dim3 grid((unsigned)tiles, (unsigned)groups);
     if constexpr (std::is_same_v<Epi, EpiLinear>) {
 #define CADENCE_BIG_ACT(ACT_)                                                          \
-  if (bm224) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 1, 7>), grid,     \
+  if (rows == 160) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 1, 5>), grid, \
+                             dim3(512), 0, st, A, lda, W, ldw, (int)M, (int)N, (int)K,  \
+                             a_goff, w_goff, EpiLinearA<ACT_>{epi});                    \
+  else if (rows == 192) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 1, 6>), grid, \
+                             dim3(512), 0, st, A, lda, W, ldw, (int)M, (int)N, (int)K,  \
+                             a_goff, w_goff, EpiLinearA<ACT_>{epi});                    \
+  else if (rows == 224) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 1, 7>), grid, \
                              dim3(512), 0, st, A, lda, W, ldw, (int)M, (int)N, (int)K,  \
                              a_goff, w_goff, EpiLinearA<ACT_>{epi});                    \
   else if (p8) hipLaunchKernelGGL((gemm_big_kernel<EpiLinearA<ACT_>, 1>), grid,         \
@@ -1688,7 +1706,13 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
         default: return (int)hipErrorInvalidValue;
       }
 #undef CADENCE_BIG_ACT
-    } else if (bm224) {
+    } else if (rows == 160) {
+      hipLaunchKernelGGL((gemm_big_kernel<Epi, 1, 5>), grid, dim3(512), 0, st, A, lda, W,
+                         ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
+    } else if (rows == 192) {
+      hipLaunchKernelGGL((gemm_big_kernel<Epi, 1, 6>), grid, dim3(512), 0, st, A, lda, W,
+                         ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
+    } else if (rows == 224) {
       hipLaunchKernelGGL((gemm_big_kernel<Epi, 1, 7>), grid, dim3(512), 0, st, A, lda, W,
                          ldw, (int)M, (int)N, (int)K, a_goff, w_goff, epi);
     } else if (p8) {

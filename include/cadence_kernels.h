@@ -76,7 +76,7 @@ int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
                                      int64_t groups);
 
 /* Output-tile height (rows) the prefill GEMM engine uses for (M, N, K,
- * groups): 256 or 224; 0 when M is small enough for the decode engines.
+ * groups): 256, 224, 192 or 160; 0 when M is small enough for the decode engines.
  * Host-only arithmetic (profiling / kernel-name bookkeeping). */
 int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups);
 
