@@ -24,8 +24,11 @@ KEYS = {
         2 * (10208 * 2560 + 2 * 7680 * 2560 + 10208 * 7680),
         "A (M x K) + W (2F x K) + out (M x F), bf16"),
     "gemm_stream_kernel<32, 10, 1, EpiGatedGelu> (decode)": (
-        r"gemm_stream_kernel<32, 10, 1, [^>]*EpiGatedGelu>", 79134720,
+        r"gemm_stream_kernel<32, 10, 1, [^>]*EpiGatedGelu[^>]*>", 79134720,
         "2F x K bf16 weights + activations + out"),
+    "gemm_stream_kernel<32, 10, 2, EpiResidRows> (decode)": (
+        r"gemm_stream_kernel<32, 10, 2, [^>]*EpiResidRows[^>]*>", 2560 * 7680 * 2,
+        "N x K bf16 weights (down projection; activations, slabs, out extra)"),
 }
 
 
