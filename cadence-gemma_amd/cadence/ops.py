@@ -153,8 +153,12 @@ def _tile(M: int) -> bool:
 def _big_key(epi: str, M: int, N: int, K: int, groups: int = 1) -> str:
   """The rocprof name of the prefill GEMM kernel a launch runs:
   gemm_big_kernel<Epi, P8, MR> (tile height 32 MR, cadence_gemm_tile_rows)."""
-  rows = _lib.load().cadence_gemm_tile_rows(M, N, K, groups)
+  lib = _lib.load()
+  rows = lib.cadence_gemm_tile_rows(M, N, K, groups)
   p8 = 1 if K % 128 == 0 else 0
+  sk = lib.cadence_gemm_big_splits(M, N, K, groups)
+  if sk > 1:   # split-K launch pair: partial GEMM + the epilogue's reduce
+    return f"gemm_big_kernel<EpiPartial, {p8}, {rows // 32}> + splitk_reduce<{epi}> (split {sk})"
   return f"gemm_big_kernel<{epi}, {p8}, {rows // 32}>"
 
 

@@ -224,6 +224,22 @@ struct EpiResidRows : EpiLinear {
   }
 };
 
+// Raw fp32 dot products of one K split -- the split is the prefill engine's
+// group index g -- to parts[g][m][n]: the split-K form of the prefill
+// engine for small M (splitk_reduce_kernel then applies the real epilogue
+// to the split-order sums).  Paired epilogues' packed gate / up columns are
+// written as they are; the reduce kernel pairs them.
+struct EpiPartial {
+  static constexpr bool kPaired = false;
+  static constexpr bool kStaged = false;
+  static constexpr bool kTile = false;
+  float* parts;
+  int64_t M, N;
+  CADENCE_DEV void apply(int64_t m, int n, float v, int g) const {
+    parts[((int64_t)g * M + m) * N + n] = v;
+  }
+};
+
 // Decode q|k|v projection with RoPE in the epilogue (stream engine, M <= 32).
 // The weight rows are pre-permuted so that each rotation pair (dims i and
 // i + hd/4 of the rotated half of a q or k head) sits in adjacent columns
@@ -1658,6 +1674,28 @@ int big_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
   return best;
 }
 
+// K splits of the prefill engine when its output tiles would leave most CUs
+// idle (one image / one prompt: M = 261..319 rows give 2 x N/256 tiles):
+// the largest S <= 8 with tiles x S <= CUs whose split length is a whole
+// number of >= 2 K-tile pairs (the 8-phase loop's unit, 128).  Ungrouped
+// launches only; 1 = no split.
+int big_splits(int64_t M, int64_t N, int64_t K, int64_t groups, int rows) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    return n;
+  }();
+  if (groups != 1 || rows == 0) return 1;
+  const int64_t tiles = ((M + rows - 1) / rows) * ((N + 255) / 256);
+  if (tiles * 2 > cus) return 1;
+  for (int sp = 8; sp >= 2; --sp)
+    if (tiles * sp <= cus && K % (128 * sp) == 0 && K / sp >= 256) return sp;
+  return 1;
+}
+
 template <class Epi>
 int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                 int64_t N, int64_t K, int64_t groups, int64_t a_goff,
@@ -1680,6 +1718,31 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
     const bool p8 = rows != 0;
     const int64_t bm = p8 ? rows : 256;
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + 255) / 256);
+    const int sk = big_splits(M, N, K, groups, rows);
+    if (sk > 1 && ws && ws_bytes >= (int64_t)sk * M * N * 4) {
+      // split-K: split s = group s (A and W advance klen columns per
+      // group), raw fp32 partials, then the epilogue on the split-order sums
+      const int64_t klen = K / sk;
+      float* parts = static_cast<float*>(ws);
+      const EpiPartial ep{parts, M, N};
+      const dim3 sgrid((unsigned)tiles, (unsigned)sk);
+#define CADENCE_BIG_PART(MR_)                                                              \
+  hipLaunchKernelGGL((gemm_big_kernel<EpiPartial, 1, MR_>), sgrid, dim3(512), 0, st, A, lda, \
+                     W, ldw, (int)M, (int)N, (int)klen, klen, klen, ep)
+      switch (rows) {
+        case 160: CADENCE_BIG_PART(5); break;
+        case 192: CADENCE_BIG_PART(6); break;
+        case 224: CADENCE_BIG_PART(7); break;
+        default: CADENCE_BIG_PART(8); break;
+      }
+#undef CADENCE_BIG_PART
+      int64_t outs = M * N;
+      int rblocks = (int)((outs + 255) / 256);
+      if (rblocks > 4096) rblocks = 4096;
+      hipLaunchKernelGGL((splitk_reduce_kernel<Epi>), dim3(rblocks, 1), dim3(256), 0, st,
+                         parts, sk, 1, (int)M, (int)N, epi);
+      return (int)hipGetLastError();
+    }
     dim3 grid((unsigned)tiles, (unsigned)groups);
     if constexpr (std::is_same_v<Epi, EpiLinear>) {
 #define CADENCE_BIG_ACT(ACT_)                                                          \
@@ -1777,6 +1840,12 @@ extern "C" {
 
 int cadence_abi_version(void) { return 11; }
 
+int cadence_gemm_big_splits(int64_t M, int64_t N, int64_t K, int64_t groups) {
+  if (M <= kSkinnyMaxM || M <= 0) return 1;
+  const int64_t g = groups > 0 ? groups : 1;
+  return big_splits(M, N, K, g, big_tile_rows(M, N, K, g));
+}
+
 int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
   if (M <= kSkinnyMaxM || M <= 0) return 0;
   const int r = big_tile_rows(M, N, K, groups > 0 ? groups : 1);
@@ -1785,6 +1854,10 @@ int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
 
 int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
                                      int64_t groups) {
+  if (M > kSkinnyMaxM) {
+    const int sk = big_splits(M, N, K, groups, big_tile_rows(M, N, K, groups));
+    return sk > 1 ? (int64_t)sk * M * N * 4 : 0;
+  }
   int ksw = 0, ss = 0;
   if (M > 0 && stream_plan(M, K, &ksw, &ss))
     return ss > 1 ? (int64_t)ss * groups * M * N * 4 : 0;

@@ -80,6 +80,13 @@ int64_t cadence_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K,
  * Host-only arithmetic (profiling / kernel-name bookkeeping). */
 int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups);
 
+/* K splits the prefill GEMM engine uses for (M, N, K, groups): > 1 when its
+ * output tiles would leave most CUs idle (small M: one image / one prompt),
+ * then gemm_big_kernel<EpiPartial, ...> writes fp32 split partials to the
+ * workspace (cadence_gemm_workspace_bytes) and splitk_reduce_kernel applies
+ * the epilogue to the split-order sums.  Host-only arithmetic. */
+int cadence_gemm_big_splits(int64_t M, int64_t N, int64_t K, int64_t groups);
+
 /* ---- GEMMs with fused epilogues ---------------------------------------- */
 
 /* out[map(m), n] = act(A[m,:] . W[n,:] + bias[n]) (+ resid[map(m), n])
