@@ -153,3 +153,25 @@ def test_positions_and_sampler_prompt_layout():
   from cadence.sampler import prompt_positions
   pos = prompt_positions(torch.tensor([3, 5]), 5)
   assert pos.tolist() == [[-1, -1, 0, 1, 2], [0, 1, 2, 3, 4]]
+
+
+def test_prefill_gemm_plan_host_arithmetic():
+  """The prefill engine's tile height and K-split plan (host-only; 256 CUs
+  assumed when no GPU is visible): bench shapes keep one pass with the tile
+  heights DESIGN §4 names, one-image / one-prompt shapes split K."""
+  lib = _lib.load()
+  rows = lib.cadence_gemm_tile_rows
+  assert rows(32 * 319, 15360, 2560, 1) == 224        # Griffin gated MLP
+  assert rows(32 * 319, 2560, 7680, 1) == 224         # Griffin down projection
+  assert rows(32 * 261, 1024, 1024, 1) == 160         # DINO attention proj
+  assert rows(32 * 256, 1152, 1152, 1) == 192         # SigLIP attention proj
+  assert rows(32 * 261, 4096, 1024, 1) == 192         # DINO fc1
+  splits = lib.cadence_gemm_big_splits
+  assert splits(32 * 319, 15360, 2560, 1) == 1
+  assert splits(32 * 261, 1024, 1024, 1) == 1
+  assert splits(261, 3072, 1024, 1) == 4               # C3 ViT qkv: K 1024
+  assert splits(319, 2560, 7680, 1) == 6               # C3 down projection
+  assert splits(319, 15360, 2560, 1) == 2              # C3 gated MLP
+  assert splits(319, 2560, 2560, 8) == 1               # grouped launches never split
+  s = splits(319, 2560, 7680, 1)
+  assert lib.cadence_gemm_workspace_bytes(319, 2560, 7680, 1) == s * 319 * 2560 * 4
