@@ -1202,6 +1202,120 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
   }
 }
 
+// Decode gated up-projection (17..32 packed rows, fragment-packed W, one K
+// split): TWO gate / up pairs -- 64 packed columns, 32 features -- per
+// workgroup, so F = 7680 takes 240 workgroups, one round on the CUs (the
+// one-pair stream kernel needs 480: two rounds, each paying the memory
+// latency once), and each wave streams its KSW k-steps in chunks of CH with
+// INF chunks of weight + activation fragments in flight: chunk c + INF's
+// loads go out right after chunk c's MFMAs, into the registers those just
+// released (a sched_barrier pins that order; the scheduler otherwise sinks
+// loads to their first use).  Cold-weight lab (tools/gemv_lab.hip): 17.2 ->
+// 14.0 us on the 2F = 15360, K = 2560 shape.  Same products and fixed-order
+// LDS reduction as gemm_stream_kernel; NORM as there.
+template <int KSW, int CH, int INF, bool NORM>
+__global__ __launch_bounds__(512) void gemm_gated_pipe_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, int M, int K,
+    EpiGatedGelu epi, float neps) {
+  constexpr int MS = 32, MR = 2, NREP = 4, NC = KSW / CH;
+  static_assert(KSW % CH == 0 && INF <= NC, "chunking");
+  __shared__ float red[8][MS * 16 * NREP];
+  __shared__ float nss[NORM ? 8 : 1][MS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int grp = blockIdx.x;               // 64-row group: 32 features
+  // epilogue operands first: thread t owns row t / 16, features
+  // grp * 32 + h * 16 + t % 16 (h = 0, 1)
+  const int pm = min((int)(threadIdx.x >> 4), M - 1);
+  EpiGatedGelu::Pref pf[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    pf[h] = epi.prefetch2(pm, grp * 32 + h * 16 + (threadIdx.x & 15), 0);
+  const u16* zpage = reinterpret_cast<const u16*>(kZeroPage + lane);
+  const int ks32 = K >> 5;
+  uint4 wb[INF][CH][NREP], xa[INF][CH][MR];
+  auto issue = [&](int c, int slot) {
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int k = (wave + 8 * (c * CH + u)) * 32;
+      const bool ok = k < K;
+#pragma unroll
+      for (int j = 0; j < NREP; ++j)   // gate halves 0 / 1, up halves 0 / 1
+        wb[slot][u][j] = ld16_nt(ok ? W + (((int64_t)(grp * 4 + j) * ks32 + (k >> 5)) * 64 + lane) * 8
+                                    : zpage);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        xa[slot][u][i] = ld16(ok ? A + ((((int64_t)(k >> 5) * MR + i) * 64 + lane) << 3) : zpage);
+    }
+  };
+  f32x4 acc[MR][NREP];
+  [[maybe_unused]] f32x4 dg[MR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    dg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int c = 0; c < INF; ++c) issue(c, c);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int slot = c % INF;
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        const bf16x8 af = __builtin_bit_cast(bf16x8, xa[slot][u][i]);
+#pragma unroll
+        for (int j = 0; j < NREP; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              af, __builtin_bit_cast(bf16x8, wb[slot][u][j]), acc[i][j], 0, 0, 0);
+        if constexpr (NORM) dg[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, af, dg[i], 0, 0, 0);
+      }
+    if (c + INF < NC) issue(c + INF, slot);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (NORM) {
+    const int r4 = lane & 3;
+    if (((lane & 15) >> 2) == (lane >> 4)) {
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        nss[wave][i * 16 + (lane & 15)] =
+            r4 == 0 ? dg[i][0] : r4 == 1 ? dg[i][1] : r4 == 2 ? dg[i][2] : dg[i][3];
+    }
+  }
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[wave][((i * 16 + rsub + r) * NREP + j) * 16 + csub] = acc[i][j][r];
+  __syncthreads();
+  const int m = threadIdx.x >> 4, c = threadIdx.x & 15;
+  if (m >= M) return;
+  float rs = 1.0f;
+  if constexpr (NORM) {
+    const float ss = ((nss[0][m] + nss[1][m]) + (nss[2][m] + nss[3][m])) +
+                     ((nss[4][m] + nss[5][m]) + (nss[6][m] + nss[7][m]));
+    const float var = rbf(ss / (float)K);
+    rs = rbf(1.0f / sqrtf(rbf(var + neps)));
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float v[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {   // p = 0 gate, 1 up
+      const int idx = (m * NREP + 2 * p + h) * 16 + c;
+      v[p] = ((red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx])) +
+             ((red[4][idx] + red[5][idx]) + (red[6][idx] + red[7][idx]));
+      if constexpr (NORM) v[p] *= rs;
+    }
+    epi.apply2_pf(m, grp * 32 + h * 16 + c, v[0], v[1], 0, pf[h]);
+  }
+}
+
 // torch.argmax order: NaN beats every number, ties (and NaN vs NaN) go to
 // the lowest index -- a NaN row still yields an index inside the vocabulary
 CADENCE_DEV bool argmax_better(float ov, int oi, float v, int i) {
@@ -2035,6 +2149,20 @@ int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
   EpiGatedGelu epi{static_cast<u16*>(out), ldo,
                    static_cast<const u16*>(bias_gate),
                    static_cast<const u16*>(bias_up), (int)((M + 15) / 16)};
+  if (M > 16 && M <= 32 && ldw == 0 && lda == 0 && K % 32 == 0 && K <= 2560) {
+    // decode, 17..32 rows: the two-pair pipelined kernel (one round)
+    const dim3 grid((unsigned)(F / 32));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const u16* a = static_cast<const u16*>(A);
+    const u16* w = static_cast<const u16*>(Wpacked);
+    if (norm)
+      hipLaunchKernelGGL((gemm_gated_pipe_kernel<10, 2, 3, true>), grid, dim3(512), 0, st, a,
+                         w, (int)M, (int)K, epi, norm_eps);
+    else
+      hipLaunchKernelGGL((gemm_gated_pipe_kernel<10, 2, 3, false>), grid, dim3(512), 0, st, a,
+                         w, (int)M, (int)K, epi, 0.0f);
+    return (int)hipGetLastError();
+  }
   return launch_gemm(static_cast<const u16*>(A), lda,
                      static_cast<const u16*>(Wpacked), ldw, M, 2 * F, K, 1, 0, 0,
                      epi, workspace, ws_bytes, static_cast<hipStream_t>(stream),

@@ -145,3 +145,19 @@ def test_pending_norm_rows_materialise_for_other_consumers(dev):
   lazy, normed, _ = _rows(dev, 32, g)
   w = rnd(512, 2560, scale=2560 ** -0.5, gen=g).to(dev)
   assert torch.equal(ops.linear(lazy, w), ops.linear(normed, w))
+
+
+@pytest.mark.parametrize("m", [32, 20])
+def test_gated_pipe_kernel_matches_stream_kernel(dev, m):
+  """The two-pair pipelined decode up-projection (packed rows, 17..32 rows)
+  sums in the one-pair stream kernel's order: bit-identical outputs at the
+  2B model's shape (F = 7680, K = 2560)."""
+  g = torch.Generator().manual_seed(61)
+  f, k = 7680, 2560
+  x = rnd(m, k, gen=g).to(dev)
+  wp = rnd(2 * f, k, scale=k ** -0.5, gen=g).to(dev)
+  bg = rnd(f, scale=0.1, gen=g).to(dev)
+  bu = rnd(f, scale=0.1, gen=g).to(dev)
+  got = ops.gated_gelu(ops.pack_rows(x), wp, bg, bu)          # pipelined kernel
+  want = ops.gated_gelu(x, wp, bg, bu, packed_out=False)       # row-major A: stream kernel
+  assert torch.equal(got.unpack(), want)

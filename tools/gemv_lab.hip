@@ -91,6 +91,80 @@ __global__ __launch_bounds__(512) void lab_gemv(const u16* __restrict__ A,
   }
 }
 
+// Pipelined core: each wave walks its KSW k-steps in chunks of CH k-steps and
+// keeps INF chunks of weight + activation fragments in flight; chunk c +
+// INF's loads are issued right after chunk c's MFMAs (the registers they
+// overwrite are free then), so one workgroup streams its whole slice with a
+// bounded register budget -- NREP = 4 column tiles (240 workgroups on the
+// gated shape: one round) instead of 2 (480: two rounds).
+template <int KSW, int NREP, int CH, int INF>
+__global__ __launch_bounds__(512) void lab_pipe_gemv(const u16* __restrict__ A,
+                                                     const u16* __restrict__ W, int N, int K,
+                                                     float* __restrict__ out) {
+  constexpr int MR = 2, NC = KSW / CH;
+  static_assert(KSW % CH == 0 && INF <= NC, "chunking");
+  __shared__ float red[8][32 * 16 * NREP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const u16* zpage = reinterpret_cast<const u16*>(kZeroPage + lane);
+  uint4 wb[INF][CH][NREP], xa[INF][CH][MR];
+  f32x4 acc[MR][NREP];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int c, int slot) {
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int k = (wave + 8 * (c * CH + u)) * 32;
+      const bool ok = k < K;
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        const int col = (blockIdx.x * NREP + j) * 16;
+        wb[slot][u][j] = ld16_nt(ok ? W + (((int64_t)(col >> 4) * (K >> 5) + (k >> 5)) * 64 + lane) * 8
+                                    : zpage);
+      }
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        xa[slot][u][i] = ld16(ok ? A + ((((int64_t)(k >> 5) * MR + i) * 64 + lane) << 3) : zpage);
+    }
+  };
+#pragma unroll
+  for (int c = 0; c < INF; ++c) issue(c, c);
+  // pin the issue order: the scheduler otherwise sinks loads to their first
+  // use (to save registers) and the wave has a third of the bytes in flight
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int slot = c % INF;
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NREP; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, xa[slot][u][i]), __builtin_bit_cast(bf16x8, wb[slot][u][j]),
+              acc[i][j], 0, 0, 0);
+    if (c + INF < NC) issue(c + INF, slot);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[wave][((i * 16 + rsub + r) * NREP + j) * 16 + csub] = acc[i][j][r];
+  __syncthreads();
+  for (int o = threadIdx.x; o < 32 * 16 * NREP; o += 512) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += red[w][o];
+    out[(int64_t)blockIdx.x * 32 * 16 * NREP + o] = v;
+  }
+}
+
 struct Lab {
   hipStream_t st;
   std::vector<u16*> w;
@@ -150,7 +224,7 @@ void run_stream(Lab& L, const char* name, int N, int K, int splits, const Epi& e
   const double us = time_graph(L, 60, [&](int c) {
     hipLaunchKernelGGL((gemm_stream_kernel<MS, KSW, NTW, Epi>), grid, dim3(512), 0, L.st,
                        L.x, (int64_t)0, L.w[c], (int64_t)0, 32, N, K, klen, (int64_t)0,
-                       (int64_t)0, parts, epi, 1);
+                       (int64_t)0, parts, epi, 1, nullptr, 0.0f);
     if (with_reduce && splits > 1) {
       int rb = (32 * N + 255) / 256;
       hipLaunchKernelGGL((splitk_reduce_kernel<Epi>), dim3(rb, 1), dim3(256), 0, L.st,
@@ -169,6 +243,16 @@ void run_lab(Lab& L, const char* name, int N, int K, int splits) {
   const double us = time_graph(L, 60, [&](int c) {
     hipLaunchKernelGGL((lab_gemv<KSW, NREP, MODE>), grid, dim3(512), 0, L.st, L.x, L.w[c],
                        N, K, klen, L.parts);
+  });
+  report(name, us, (int64_t)N * K * 2);
+}
+
+template <int KSW, int NREP, int CH, int INF>
+void run_pipe(Lab& L, const char* name, int N, int K) {
+  dim3 grid(N / 16 / NREP);
+  const double us = time_graph(L, 60, [&](int c) {
+    hipLaunchKernelGGL((lab_pipe_gemv<KSW, NREP, CH, INF>), grid, dim3(512), 0, L.st, L.x,
+                       L.w[c], N, K, L.parts);
   });
   report(name, us, (int64_t)N * K * 2);
 }
@@ -203,59 +287,24 @@ int main() {
   CK(hipMemset(L.bias, 0, 15360 * 2));
 
   printf("== pure streaming read (nt 16-B loads)\n");
-  for (int64_t mb : {13, 26, 39, 79}) {
-    const int64_t bytes = mb == 13 ? 2560LL * 2560 * 2 : mb == 26 ? 5120LL * 2560 * 2
-                        : mb == 39 ? 2560LL * 7680 * 2 : 15360LL * 2560 * 2;
-    for (int blocks : {512, 1024, 2048}) {
-      char nm[96];
-      snprintf(nm, sizeof nm, "read %lld MB, %d blocks x 256", (long long)(bytes >> 20), blocks);
-      run_read(L, nm, bytes, blocks);
-    }
+  for (int blocks : {1024, 2048}) {
+    char nm[96];
+    snprintf(nm, sizeof nm, "read 79 MB, %d blocks x 256", blocks);
+    run_read(L, nm, 15360LL * 2560 * 2, blocks);
   }
-
   EpiGatedGelu gg{L.out, 0, L.bias, L.bias, 2};
   printf("== gated up-projection N=15360 (2F) K=2560\n");
   run_stream<32, 10, 1>(L, "stream<32,10,1,Gated> s1 (shipped)", 15360, 2560, 1, gg, false);
-  run_stream<32, 5, 1>(L, "stream<32,5,1,Gated> s2 raw partials", 15360, 2560, 2, gg, false);
-  run_stream<32, 5, 1>(L, "stream<32,5,1,Gated> s2 + reduce", 15360, 2560, 2, gg, true);
-  run_stream<32, 4, 1>(L, "stream<32,4,1,Gated> s3 raw partials", 15360, 2560, 3, gg, false);
-  run_stream<32, 3, 1>(L, "stream<32,3,1,Gated> s4 raw partials", 15360, 2560, 4, gg, false);
-
-  EpiLinear el{L.out, 0, nullptr, nullptr, 0, 0, RowMap{1 << 30, 0, 0}, 0.f};
-  printf("== down-projection N=2560 K=7680\n");
-  run_stream<32, 10, 2>(L, "stream<32,10,2> s3 raw (shipped)", 2560, 7680, 3, el, false);
-  run_stream<32, 10, 1>(L, "stream<32,10,1> s3 raw", 2560, 7680, 3, el, false);
-  run_stream<32, 5, 2>(L, "stream<32,5,2> s6 raw", 2560, 7680, 6, el, false);
-  run_stream<32, 5, 1>(L, "stream<32,5,1> s6 raw", 2560, 7680, 6, el, false);
-  run_stream<32, 4, 1>(L, "stream<32,4,1> s8 raw", 2560, 7680, 8, el, false);
-  printf("== y|x projection N=5120 K=2560\n");
-  run_stream<32, 10, 2>(L, "stream<32,10,2> s1 (shipped)", 5120, 2560, 1, el, false);
-  run_stream<32, 10, 1>(L, "stream<32,10,1> s1", 5120, 2560, 1, el, false);
-  run_stream<32, 5, 2>(L, "stream<32,5,2> s2 raw", 5120, 2560, 2, el, false);
-  run_stream<32, 5, 1>(L, "stream<32,5,1> s2 raw", 5120, 2560, 2, el, false);
-  run_stream<32, 4, 1>(L, "stream<32,4,1> s3 raw", 5120, 2560, 3, el, false);
-  printf("== output projection N=2560 K=2560\n");
-  run_stream<32, 5, 2>(L, "stream<32,5,2> s2 raw (shipped)", 2560, 2560, 2, el, false);
-  run_stream<32, 5, 1>(L, "stream<32,5,1> s2 raw", 2560, 2560, 2, el, false);
-  run_stream<32, 10, 1>(L, "stream<32,10,1> s1", 2560, 2560, 1, el, false);
-  run_stream<32, 4, 1>(L, "stream<32,4,1> s3 raw", 2560, 2560, 3, el, false);
-  run_stream<32, 3, 1>(L, "stream<32,3,1> s4 raw", 2560, 2560, 4, el, false);
-  printf("== lab core, gated shape N=15360 K=2560\n");
-  run_lab<10, 2, 0>(L, "lab<10,2> act+w s1", 15360, 2560, 1);
-  run_lab<10, 2, 1>(L, "lab<10,2> w only s1", 15360, 2560, 1);
-  run_lab<10, 2, 2>(L, "lab<10,2> w only no-mfma s1", 15360, 2560, 1);
-  run_lab<5, 2, 0>(L, "lab<5,2> act+w s2", 15360, 2560, 2);
-  run_lab<5, 2, 1>(L, "lab<5,2> w only s2", 15360, 2560, 2);
-  run_lab<5, 4, 0>(L, "lab<5,4> act+w s2", 15360, 2560, 2);
-  run_lab<5, 4, 1>(L, "lab<5,4> w only s2", 15360, 2560, 2);
-  run_lab<3, 4, 0>(L, "lab<3,4> act+w s4", 15360, 2560, 4);
-  run_lab<2, 4, 0>(L, "lab<2,4> act+w s5", 15360, 2560, 5);
-  run_lab<10, 1, 0>(L, "lab<10,1> act+w s1", 15360, 2560, 1);
-  printf("== lab core, down shape N=2560 K=7680\n");
-  run_lab<10, 2, 0>(L, "lab<10,2> act+w s3", 2560, 7680, 3);
-  run_lab<10, 2, 1>(L, "lab<10,2> w only s3", 2560, 7680, 3);
-  run_lab<5, 4, 0>(L, "lab<5,4> act+w s6", 2560, 7680, 6);
-  run_lab<3, 4, 0>(L, "lab<3,4> act+w s10", 2560, 7680, 10);
+  run_lab<10, 2, 0>(L, "lab<10,2> act+w s1 (all loads up front)", 15360, 2560, 1);
+  run_pipe<10, 2, 2, 3>(L, "pipe<10,2> chunk 2 x 3 in flight (480 wg)", 15360, 2560);
+  run_pipe<10, 4, 2, 3>(L, "pipe<10,4> chunk 2 x 3 in flight (240 wg)", 15360, 2560);
+  run_pipe<10, 4, 2, 4>(L, "pipe<10,4> chunk 2 x 4 in flight (240 wg)", 15360, 2560);
+  run_pipe<10, 4, 1, 6>(L, "pipe<10,4> chunk 1 x 6 in flight (240 wg)", 15360, 2560);
+  run_pipe<10, 4, 5, 2>(L, "pipe<10,4> chunk 5 x 2 in flight (240 wg)", 15360, 2560);
+  run_pipe<10, 6, 2, 3>(L, "pipe<10,6> chunk 2 x 3 in flight (160 wg)", 15360, 2560);
+  printf("== down-projection shape N=2560 K=2560 split slice (one K split of 7680)\n");
+  run_lab<10, 2, 0>(L, "lab<10,2> act+w s1 (80 wg)", 2560, 2560, 1);
+  run_pipe<10, 2, 2, 3>(L, "pipe<10,2> chunk 2 x 3 (80 wg)", 2560, 2560);
   printf("done\n");
   return 0;
 }
