@@ -795,14 +795,21 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
       __builtin_amdgcn_global_load_lds((gptr_t)(p1 + k0), (lptr_t)(dst + 64), 16, 0, 0);
     };
     const int xr = lane & 7;   // row & 7 of every fragment row this lane reads
+    // Each phase's fragments are read one phase ahead where the data is
+    // already retired: B-h1 with phase 1's reads (b1 is idle in phase 1),
+    // and -- given the registers for a second A set (MR < 8) -- A-h1 in
+    // phase 2, so phases 2-4 (6-8) start their MFMAs on fragments already in
+    // registers and only phases 1 and 5 wait for the LDS.
+    constexpr bool PFA = MR < 8;
     bf16x8 af[4][2], b0[2][2], b1[2][2];
-    auto readA = [&](int buf, int mh) {
+    [[maybe_unused]] bf16x8 ag[4][2];
+    auto readA = [&](int buf, int mh, bf16x8 (&a)[4][2], int i0 = 0, int i1 = 4) {
       const uint4* base = &smem[(buf * 4 + mh) * HT];
 #pragma unroll
-      for (int i = 0; i < (mh ? MR - 4 : 4); ++i)
+      for (int i = i0; i < min(i1, mh ? MR - 4 : 4); ++i)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          af[i][ks] = __builtin_bit_cast(
+          a[i][ks] = __builtin_bit_cast(
               bf16x8, base[(wm * 64 + i * 16 + (lane & 15)) * 8 +
                            ((ks * 4 + (lane >> 4)) ^ xr)]);
     };
@@ -816,18 +823,55 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
               bf16x8, base[(wn * 32 + j * 16 + (lane & 15)) * 8 +
                            ((ks * 4 + (lane >> 4)) ^ xr)]);
     };
-    auto mma = [&](int mh, int nh, const bf16x8 (&bf)[2][2]) {
-      __builtin_amdgcn_s_setprio(1);
+    auto mma_rows = [&](int mh, int nh, const bf16x8 (&a)[4][2], const bf16x8 (&bf)[2][2],
+                        int i0, int i1) {
 #pragma unroll
-      for (int i = 0; i < (mh ? MR - 4 : 4); ++i)
+      for (int i = i0; i < i1; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
             acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                af[i][ks], bf[j][ks], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+                a[i][ks], bf[j][ks], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+    };
+    auto mma = [&](int mh, int nh, const bf16x8 (&a)[4][2], const bf16x8 (&bf)[2][2]) {
+      __builtin_amdgcn_s_setprio(1);
+      mma_rows(mh, nh, a, bf, 0, mh ? MR - 4 : 4);
       __builtin_amdgcn_s_setprio(0);
     };
+    // The compiler waits for every outstanding LDS read (lgkmcnt(0)) before
+    // the first MFMA that consumes one, so a read meant for a later phase
+    // goes out AFTER the wait of the phase it is issued in: behind the
+    // quadrant's first MFMAs (sched_barrier keeps it there).
+    // Phases 1 / 5 (fragments retired only by the previous barrier): rows
+    // 0-1 of A-h0 + B-h0, their 8 MFMAs, then rows 2-3 + B-h1 (phase 2's).
+    auto quad0 = [&](int buf) {
+      readA(buf, 0, af, 0, 2);
+      readB(buf, 0, b0);
+      __builtin_amdgcn_s_setprio(1);
+      mma_rows(0, 0, af, b0, 0, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      readA(buf, 0, af, 2, 4);
+      readB(buf, 1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_rows(0, 0, af, b0, 2, 4);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    // Phases 2 / 6: with a second A set, A-h1 (phase 3's) behind row 0.
+    auto quad1 = [&](int buf) {
+      __builtin_amdgcn_s_setprio(1);
+      if constexpr (PFA) {
+        mma_rows(0, 1, af, b1, 0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        readA(buf, 1, ag);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_rows(0, 1, af, b1, 1, 4);
+      } else {
+        mma_rows(0, 1, af, b1, 0, 4);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto& a1 = PFA ? ag : af;   // the A-h1 fragments
     const int nk = K / BK;
     // prologue: even <- tile 0 (all four), odd <- tile 1 (A-h0, B-h0, B-h1)
     stage(0, 0, sa[0][0], sa[0][1], 0);
@@ -843,18 +887,15 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
       const int kO1 = (2 * it + 1) * BK, kE = (2 * it + 2) * BK, kO = (2 * it + 3) * BK;
       const bool more = 2 * it + 2 < nk;         // tiles 2i+2 and 2i+3 exist
       // phase 1
-      readA(0, 0);
-      readB(0, 0, b0);
       stage(1, 1, sa[1][0], sa[1][1], kO1);
-      mma(0, 0, b0); p8_barrier();
+      quad0(0); p8_barrier();
       // phase 2
-      readB(0, 1, b1);
       if (more) stage(0, 0, sa[0][0], sa[0][1], kE);
-      mma(0, 1, b1); p8_barrier();
+      quad1(0); p8_barrier();
       // phase 3
-      readA(0, 1);
+      if constexpr (!PFA) readA(0, 1, af);
       if (more) stage(0, 2, sb[0][0], sb[0][1], kE);
-      mma(1, 1, b1); p8_barrier();
+      mma(1, 1, a1, b1); p8_barrier();
       // phase 4
       if (more) {
         stage(0, 3, sb[1][0], sb[1][1], kE);
@@ -862,20 +903,17 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      mma(1, 0, b0); p8_barrier();
+      mma(1, 0, a1, b0); p8_barrier();
       // phase 5
-      readA(1, 0);
-      readB(1, 0, b0);
       if (more) stage(0, 1, sa[1][0], sa[1][1], kE);
-      mma(0, 0, b0); p8_barrier();
+      quad0(1); p8_barrier();
       // phase 6
-      readB(1, 1, b1);
       if (more) stage(1, 0, sa[0][0], sa[0][1], kO);
-      mma(0, 1, b1); p8_barrier();
+      quad1(1); p8_barrier();
       // phase 7
-      readA(1, 1);
+      if constexpr (!PFA) readA(1, 1, af);
       if (more) stage(1, 2, sb[0][0], sb[0][1], kO);
-      mma(1, 1, b1); p8_barrier();
+      mma(1, 1, a1, b1); p8_barrier();
       // phase 8
       if (more) {
         stage(1, 3, sb[1][0], sb[1][1], kO);
@@ -883,7 +921,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      mma(1, 0, b0); p8_barrier();
+      mma(1, 0, a1, b0); p8_barrier();
     }
   } else {
   // 2-buffer schedule: wave w moves pieces 8w..8w+7 of the 64 pieces of a

@@ -34,8 +34,12 @@ def main():
                            "8192x4352x1152").split(",")]
   tag = "big"
   for M, N, K in shapes:
-    a = torch.randn(M, K, device=dev).to(BF)
-    w = (torch.randn(N, K, device=dev) / K ** .5).to(BF)
+    if os.environ.get("UNIFORM") == "1":   # uniform [-1, 1) operands
+      a = (torch.rand(M, K, device=dev) * 2 - 1).to(BF)
+      w = (torch.rand(N, K, device=dev) * 2 - 1).to(BF)
+    else:
+      a = torch.randn(M, K, device=dev).to(BF)
+      w = (torch.randn(N, K, device=dev) / K ** .5).to(BF)
     out = torch.empty(M, N, device=dev, dtype=BF)
     us = timeit(lambda: ops.linear(a, w, out=out))
     print(f"{tag:6s} M={M:6d} N={N:6d} K={K:5d} {us:8.1f} us "
