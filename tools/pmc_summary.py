@@ -23,8 +23,8 @@ KEYS = {
         r"gemm_big_kernel<[^>]*EpiGatedGelu, 1, 7>",
         2 * (10208 * 2560 + 2 * 7680 * 2560 + 10208 * 7680),
         "A (M x K) + W (2F x K) + out (M x F), bf16"),
-    "gemm_stream_kernel<32, 10, 1, EpiGatedGelu> (decode)": (
-        r"gemm_stream_kernel<32, 10, 1, [^>]*EpiGatedGelu[^>]*>", 79134720,
+    "gemm_gated_pipe_kernel<10, 2, 3, true> (decode)": (
+        r"gemm_gated_pipe_kernel<10, 2, 3, true>", 79134720,
         "2F x K bf16 weights + activations + out"),
     "gemm_stream_kernel<32, 10, 2, EpiResidRows> (decode)": (
         r"gemm_stream_kernel<32, 10, 2, [^>]*EpiResidRows[^>]*>", 2560 * 7680 * 2,
