@@ -376,16 +376,24 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
     const int c0 = t * GA_KT;
     const uint4* kimg = smem + (buf * 2) * TILE;
     const uint32_t vlds = (uint32_t)(uintptr_t)(smem + (buf * 2 + 1) * TILE);
+    // every K fragment of the tile read before the first QK^T MFMA (one
+    // LDS wait instead of one per 16-key group)
+    bf16x8 kf[4][KS];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int kr = 16 * tt + c16;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        kf[tt][ks] = __builtin_bit_cast(bf16x8, kimg[kr * CPR + ((4 * ks + g) ^ (kr & 15))]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     f32x4 s[4];
 #pragma unroll
     for (int tt = 0; tt < 4; ++tt) {
       s[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int kr = 16 * tt + c16;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 kf = __builtin_bit_cast(bf16x8, kimg[kr * CPR + ((4 * ks + g) ^ (kr & 15))]);
-        s[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[tt], 0, 0, 0);
-      }
+      for (int ks = 0; ks < KS; ++ks)
+        s[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[tt][ks], qf[ks], s[tt], 0, 0, 0);
     }
     if (c0 + GA_KT > N) {              // tail tile: keys past N
 #pragma unroll
@@ -433,24 +441,55 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
       pf[kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
     }
     l += ps0 + ps1;
+    // V^T fragments by the transposing LDS read: all 2 NDT of a key half in
+    // ONE asm statement with one lgkmcnt wait (the compiler's builtin for the
+    // read is preceded by a vmcnt(0), i.e. it would wait for the next tile's
+    // DMA; a statement per pair waited once per pair)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int r1 = 32 * kk + 4 * g + tq, r2 = r1 + 16;
       const uint32_t a1 = vlds + r1 * (CPR * 16) + 8 * (tp & 1);
       const uint32_t a2 = vlds + r2 * (CPR * 16) + 8 * (tp & 1);
       const int x1 = (r1 & 7) << 1, x2 = (r2 & 7) << 1;
+      uint32_t ad[2 * NDT];
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         const int ch = 2 * dt + (tp >> 1);
-        uint2 w1, w2;
+        ad[2 * dt] = a1 + 16 * (ch ^ x1);
+        ad[2 * dt + 1] = a2 + 16 * (ch ^ x2);
+      }
+      uint2 w[2 * NDT];
+      if constexpr (NDT == 4) {
         asm volatile(
-            "ds_read_b64_tr_b16 %0, %2\n"
-            "ds_read_b64_tr_b16 %1, %3\n"
+            "ds_read_b64_tr_b16 %0, %8\n" "ds_read_b64_tr_b16 %1, %9\n"
+            "ds_read_b64_tr_b16 %2, %10\n" "ds_read_b64_tr_b16 %3, %11\n"
+            "ds_read_b64_tr_b16 %4, %12\n" "ds_read_b64_tr_b16 %5, %13\n"
+            "ds_read_b64_tr_b16 %6, %14\n" "ds_read_b64_tr_b16 %7, %15\n"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(w1), "=&v"(w2)
-            : "v"(a1 + 16 * (ch ^ x1)), "v"(a2 + 16 * (ch ^ x2))
+            : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]),
+              "=&v"(w[4]), "=&v"(w[5]), "=&v"(w[6]), "=&v"(w[7])
+            : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]),
+              "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7])
             : "memory");
-        const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(w1.x, w1.y, w2.x, w2.y));
+      } else {
+        static_assert(NDT == 5, "hd 64 / 72");
+        asm volatile(
+            "ds_read_b64_tr_b16 %0, %10\n" "ds_read_b64_tr_b16 %1, %11\n"
+            "ds_read_b64_tr_b16 %2, %12\n" "ds_read_b64_tr_b16 %3, %13\n"
+            "ds_read_b64_tr_b16 %4, %14\n" "ds_read_b64_tr_b16 %5, %15\n"
+            "ds_read_b64_tr_b16 %6, %16\n" "ds_read_b64_tr_b16 %7, %17\n"
+            "ds_read_b64_tr_b16 %8, %18\n" "ds_read_b64_tr_b16 %9, %19\n"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]),
+              "=&v"(w[5]), "=&v"(w[6]), "=&v"(w[7]), "=&v"(w[8]), "=&v"(w[9])
+            : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]),
+              "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8]), "v"(ad[9])
+            : "memory");
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const bf16x8 vf = __builtin_bit_cast(
+            bf16x8, make_uint4(w[2 * dt].x, w[2 * dt].y, w[2 * dt + 1].x, w[2 * dt + 1].y));
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[kk], o[dt], 0, 0, 0);
       }
     }
