@@ -306,16 +306,20 @@ __global__ __launch_bounds__(GA_MAXW * 64) void griffin_attn_kernel(GAArgs a) {
 // zero Q fragment, or landing in output dims that are not stored.  fp32
 // scores (the reference tower is fp32); only the tail tile is masked.
 
-template <int KS, int NDT>
+template <int KS, int NDT, int CPR, int NB>
 __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
     const u16* __restrict__ qkv, u16* __restrict__ out, int N, int H, int hd,
     float scale_log2) {
-  constexpr int CPR = 16;             // 16-B chunks per LDS row (256 B)
-  constexpr int TILE = GA_KT * CPR;   // uint4 per K or V image (16 KiB)
+  // CPR 16-B chunks per LDS row: 8 (128 B) for hd 64, 16 (256 B) for hd 72;
+  // NB tile buffers (tile t + NB - 1 is fetched while tile t is computed)
+  constexpr int TILE = GA_KT * CPR;   // uint4 per K or V image
   constexpr int NP = TILE / 64;       // 1-KiB DMA pieces per image
   constexpr int NW = 8;
-  static_assert(4 * KS <= CPR && 2 * NDT <= CPR, "row padding");
-  __shared__ __attribute__((aligned(16))) uint4 smem[2 * 2 * TILE];
+  constexpr int DPW = 2 * NP / NW;    // DMA instructions per wave per tile
+  constexpr int RPP = 64 / CPR;       // rows per DMA piece
+  static_assert(4 * KS <= CPR && 2 * NDT <= CPR && 2 * NP % NW == 0, "row padding");
+  static_assert(NB == 2 || (NB == 3 && DPW == 2), "vmcnt below");
+  __shared__ __attribute__((aligned(16))) uint4 smem[NB * 2 * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
@@ -333,16 +337,22 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
   const int64_t rs = 3 * (int64_t)D;
   const u16* base = qkv + (int64_t)b * N * rs + (int64_t)h * hd;
   const int real = hd / 8;            // stored chunks of a row
+  // V^T image swizzle (even, so a lane's two 8-B halves stay in one chunk):
+  // the 8 rows a 32-lane transposed read touches land on 8 distinct 32-B
+  // bank slots -- (r & 7) << 1 over 256-B rows, ((r >> 1) & 3) << 1 over
+  // 128-B rows (two rows per bank row)
+  auto vx = [](int r) { return CPR == 16 ? ((r & 7) << 1) : (((r >> 1) & 3) << 1); };
 
-  // DMA: piece i covers 4 rows (lane l -> row 4i + l/16, slot l%16)
-  const int drow = lane >> 4, dslot = lane & 15;
+  // DMA: piece i covers RPP rows (lane l -> row RPP i + l / CPR, slot l % CPR)
+  const int drow = lane / CPR, dslot = lane % CPR;
   auto stage = [&](int t, int buf) {
     const int c0 = t * GA_KT;
+#pragma unroll
     for (int i = wave; i < 2 * NP; i += NW) {
       const bool isv = i >= NP;
       const int pi = isv ? i - NP : i;
-      const int r = 4 * pi + drow;
-      int ch = isv ? (dslot ^ ((r & 7) << 1)) : (dslot ^ (r & 15));
+      const int r = RPP * pi + drow;
+      int ch = isv ? (dslot ^ vx(r)) : (dslot ^ (r & (CPR - 1)));
       ch = min(ch, real - 1);
       const int key = min(c0 + r, N - 1);
       const u16* src = base + key * rs + (isv ? 2 * D : D) + ch * 8;
@@ -351,7 +361,6 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
     }
   };
   const int ntiles = (N + GA_KT - 1) / GA_KT;
-  stage(0, 0);
 
   const int q0 = (qb * NW + wave) * 16;
   const int qi = min(q0 + c16, N - 1);
@@ -362,6 +371,11 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
     qf[ks] = __builtin_bit_cast(bf16x8, d < hd ? ld16(base + qi * rs + d)
                                                : make_uint4(0, 0, 0, 0));
   }
+  // q in registers before any DMA is issued, by a wait the compiler sees
+  // (otherwise it keeps the q loads pending and puts a vmcnt(0) -- a wait
+  // for every tile in flight -- before each tile's first MFMA)
+  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+  for (int t = 0; t < NB - 1 && t < ntiles; ++t) stage(t, t);
   f32x4 o[NDT];
 #pragma unroll
   for (int j = 0; j < NDT; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -369,10 +383,17 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
   constexpr float kThr = 8.0f;
   const int tq = c16 >> 2, tp = c16 & 3;
 
-  __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
+    const int buf = t % NB;
+    // tile t landed (this wave's DMA: tiles > t may stay in flight), then
+    // every wave's: raw s_barrier (__syncthreads would drain all DMA)
+    if (NB == 3 && t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // the buffer of tile t - 1, which every wave is done reading
+    if (t + NB - 1 < ntiles) stage(t + NB - 1, (t + NB - 1) % NB);
     const int c0 = t * GA_KT;
     const uint4* kimg = smem + (buf * 2) * TILE;
     const uint32_t vlds = (uint32_t)(uintptr_t)(smem + (buf * 2 + 1) * TILE);
@@ -384,7 +405,7 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
       const int kr = 16 * tt + c16;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        kf[tt][ks] = __builtin_bit_cast(bf16x8, kimg[kr * CPR + ((4 * ks + g) ^ (kr & 15))]);
+        kf[tt][ks] = __builtin_bit_cast(bf16x8, kimg[kr * CPR + ((4 * ks + g) ^ (kr & (CPR - 1)))]);
     }
     __builtin_amdgcn_sched_barrier(0);
     f32x4 s[4];
@@ -450,7 +471,7 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
       const int r1 = 32 * kk + 4 * g + tq, r2 = r1 + 16;
       const uint32_t a1 = vlds + r1 * (CPR * 16) + 8 * (tp & 1);
       const uint32_t a2 = vlds + r2 * (CPR * 16) + 8 * (tp & 1);
-      const int x1 = (r1 & 7) << 1, x2 = (r2 & 7) << 1;
+      const int x1 = vx(r1), x2 = vx(r2);
       uint32_t ad[2 * NDT];
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
@@ -493,7 +514,6 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[kk], o[dt], 0, 0, 0);
       }
     }
-    __syncthreads();
   }
   float lt = l;
   lt += __shfl_xor(lt, 16, 64);
@@ -548,10 +568,10 @@ __attribute__((visibility("hidden"))) int vit_stream_attention_launch(
   const u16* in = static_cast<const u16*>(qkv);
   u16* o = static_cast<u16*>(out);
   if (hd == 64)
-    hipLaunchKernelGGL((vit_stream_attn_kernel<2, 4>), grid, block, 0, st, in, o,
+    hipLaunchKernelGGL((vit_stream_attn_kernel<2, 4, 8, 3>), grid, block, 0, st, in, o,
                        (int)N, (int)H, (int)hd, sl2);
   else
-    hipLaunchKernelGGL((vit_stream_attn_kernel<3, 5>), grid, block, 0, st, in, o,
+    hipLaunchKernelGGL((vit_stream_attn_kernel<3, 5, 16, 2>), grid, block, 0, st, in, o,
                        (int)N, (int)H, (int)hd, sl2);
   return (int)hipGetLastError();
 }
