@@ -168,15 +168,24 @@ __global__ __launch_bounds__(GA_MAXW * 64) void griffin_attn_kernel(GAArgs a) {
     const uint4* kimg = smem + (buf * 2) * TILE;
     const uint32_t vlds = (uint32_t)(uintptr_t)(smem + (buf * 2 + 1) * TILE);
     // S^T = K . Q^T: s[tt][r] = S[key c0 + 16 tt + 4 g + r][query q0 + c16]
+    // K fragments QG k-steps at a time, each group read before its MFMAs
+    // (one LDS wait per group; the compiler otherwise waits per fragment)
+    constexpr int QG = 2;
     f32x4 s[4];
 #pragma unroll
     for (int tt = 0; tt < 4; ++tt) {
       s[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int kr = 16 * tt + c16;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 kf = __builtin_bit_cast(bf16x8, kimg[kr * CPR + ((4 * ks + g) ^ (kr & 15))]);
-        s[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[tt], 0, 0, 0);
+      for (int k0 = 0; k0 < KS; k0 += QG) {
+        bf16x8 kf[QG];
+#pragma unroll
+        for (int u = 0; u < QG; ++u)
+          kf[u] = __builtin_bit_cast(bf16x8, kimg[kr * CPR + ((4 * (k0 + u) + g) ^ (kr & 15))]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < QG; ++u)
+          s[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[u], qf[k0 + u], s[tt], 0, 0, 0);
       }
     }
     // logits: bf16-rounded dot (the scale 2^-k is exact), masked where the
