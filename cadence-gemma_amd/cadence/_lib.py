@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -32,6 +32,7 @@ _SIGS: dict[str, list] = {
     "cadence_gemm_workspace_bytes": [I64, I64, I64, I64],
     "cadence_gemm_tile_rows": [I64, I64, I64, I64],
     "cadence_gemm_big_splits": [I64, I64, I64, I64],
+    "cadence_gemm_set_engine": [I32],
     "cadence_gemm_linear": [P, I64, P, I64, P, P, I64, P, I64, I64, I64, I64,
                             I32, I64, I64, I64, P, I64, P],
     "cadence_gemm_gated_gelu": [P, I64, P, I64, P, P, P, I64, I64, I64, I64, P,
@@ -82,7 +83,7 @@ _SIGS: dict[str, list] = {
     "cadence_local_attention_cached": [P, P, P, P, P, P, P, I64, I64, I64, I64,
                                        I64, P],
     "cadence_kv_ring_update": [P, P, P, P, P, I64, I64, I64, P],
-    "cadence_decode_advance": [P, P, I64, P, P, P, P, I32, I32, I64, P],
+    "cadence_decode_advance": [P, P, I64, P, P, P, P, I32, I32, I32, I64, P],
 }
 _RESTYPE = {
     "cadence_gemm_workspace_bytes": I64,

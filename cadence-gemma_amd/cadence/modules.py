@@ -144,8 +144,9 @@ class LocalAttentionBlock(nn.Module):
         new_cache = AttentionBlockCache(ck, cv, nt)
     else:
       n_fill = min(self.window_size, t)
-      if n_fill != 1 and n_fill != self.window_size:
-        # reference modules.py:206-225 only supports 1 or >= window tokens
+      if return_cache and n_fill != 1 and n_fill != self.window_size:
+        # reference modules.py:206-225 only updates a cache with 1 or
+        # >= window tokens; it is called only when return_cache (:445-451)
         raise NotImplementedError()
       if t == 1 and tuned:
         enc = ops.local_attention_decode_(q, k, v, cache.keys, cache.values,

@@ -181,6 +181,26 @@ def _counters(dev: torch.device, n: int):
   return buf
 
 
+def claim_counters(stream: torch.cuda.Stream, owner) -> None:
+  """Ties the counter buffer of `stream` to `owner` (a captured decode graph,
+  whose kernels hold its raw pointer): the owner keeps the buffer alive, and
+  the table entry is dropped when the owner is collected, so recaptures on
+  fresh streams do not accumulate buffers.  A stream handle the pool hands
+  out again later gets a fresh zeroed buffer; kernels leave counters at zero
+  and launches on one stream never overlap, so sharing is safe either way."""
+  import weakref
+  key = (stream.device.index, stream.cuda_stream)
+  buf = _COUNTERS.get(key)
+  if buf is None:
+    return
+  owner._cadence_counters = buf
+
+  def drop(key=key, ref=weakref.ref(buf)):
+    if _COUNTERS.get(key) is ref():
+      _COUNTERS.pop(key, None)
+  weakref.finalize(owner, drop)
+
+
 def _ws(M: int, N: int, K: int, groups: int, like: torch.Tensor):
   n = _lib.load().cadence_gemm_workspace_bytes(M, N, K, groups)
   if n == 0:
@@ -1014,9 +1034,9 @@ def _splice_positions(text_pos, n_vis):
 
 @_reg("decode_advance_(Tensor next_token, Tensor(a!) tokens_out, "
       "Tensor(b!) step, Tensor(c!) positions, Tensor(d!)? cur=None, "
-      "Tensor(e!)? done=None, int eos_id=-1, int pad_id=0) -> ()")
+      "Tensor(e!)? done=None, int eos_id=-1, int pad_id=0, int eos_from=1) -> ()")
 def _decode_advance(next_token, tokens_out, step, positions, cur=None,
-                    done=None, eos_id=-1, pad_id=0):
+                    done=None, eos_id=-1, pad_id=0, eos_from=1):
   B = next_token.numel()
   _need(tokens_out.dtype == _I32 and tokens_out.stride(1) == 1, "tokens_out")
   if cur is not None:
@@ -1026,8 +1046,8 @@ def _decode_advance(next_token, tokens_out, step, positions, cur=None,
           "done must be int32[B + 1]")
   _lib.check(_lib.load().cadence_decode_advance(
       _p(next_token), _p(tokens_out), tokens_out.stride(0), _p(step),
-      _p(positions), _p(cur), _p(done), int(eos_id), int(pad_id), B,
-      _s(next_token)), "decode_advance")
+      _p(positions), _p(cur), _p(done), int(eos_id), int(pad_id),
+      int(eos_from), B, _s(next_token)), "decode_advance")
 
 
 # ----------------------------------------------------------------- helpers

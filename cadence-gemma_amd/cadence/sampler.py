@@ -15,6 +15,16 @@ Decode runs on device: soft-cap + argmax are fused into the logits kernel,
 the next token / positions / step counter are advanced by a kernel, and the
 whole step can be captured once into a hipGraph and replayed
 (`use_graph=True`), so the loop has no per-step host sync.
+
+EOS stopping (`end_sampling_at_eos_token=True`) keeps the reference's
+behaviour by default (recurrentgemma/torch/sampler.py:177-187, 209-225):
+`done_now = torch.equal(next_token, eos)` compares the batch's [B] tokens
+with a [1] tensor, so only a batch of ONE row ever stops -- after a decode
+step samples EOS (the token sampled from the prompt is never tested), the
+rest of the buffer stays pad -- and rows of a larger batch keep generating
+after their EOS.  `eos_per_row=True` opts into per-row stopping instead:
+each row is padded after its first EOS (the first token included) and the
+loop ends once every row is done.
 """
 
 from __future__ import annotations
@@ -59,12 +69,14 @@ class Sampler:
   """Sampler for a `cadence.Griffin` model."""
 
   def __init__(self, model, vocab, greedy_sampling: bool = True,
-               is_it_model: bool = False, use_graph: bool = True):
+               is_it_model: bool = False, use_graph: bool = True,
+               eos_per_row: bool = False):
     self.model = model
     self.vocab = vocab
     self.greedy_sampling = greedy_sampling
     self._is_it_model = is_it_model
     self.use_graph = use_graph
+    self.eos_per_row = eos_per_row
     self._eos_token = torch.tensor([self.vocab.eos_id()], device=self.device)
 
   @property
@@ -116,6 +128,13 @@ class Sampler:
     """
     dev = self.device
     b, t = tokens.shape
+    if not tokens.is_cuda and tokens.numel():
+      # nn.Embedding raises on an id outside [0, V) (modules.py:994-1001);
+      # the embedding kernel cannot, so host-side prompts are checked here
+      lo, hi = int(tokens.min()), int(tokens.max())
+      if lo < 0 or hi >= self.vocab_size:
+        raise ValueError(f"prompt token ids must lie in [0, {self.vocab_size}); "
+                         f"got [{lo}, {hi}]")
     pos_cpu = prompt_positions(input_lengths.cpu(), t)
     positions = pos_cpu.to(dev)
     # image tokens spliced in front by the prefill (griffin.py:179: only when
@@ -129,6 +148,8 @@ class Sampler:
       n_img = self.model.n_visual_tokens
     tokens = tokens.to(dev, torch.int32)
     steps = total_generation_steps
+    # the reference's torch.equal(next_token, eos) only ever holds for B == 1
+    eos_stop = end_sampling_at_eos_token and (self.eos_per_row or b == 1)
     if steps == 0:
       prev_logits, _ = self.apply_model(tokens, positions, None,
                                         return_logits and echo, False,
@@ -160,7 +181,7 @@ class Sampler:
         step = torch.zeros(1, dtype=torch.int32, device=dev)
         cur = tokens[:, -1].to(torch.int32).contiguous()
         done = self._decode_graph(cur, pos, cache, buf, step, steps,
-                                  end_sampling_at_eos_token, events, start=0,
+                                  eos_stop, events, start=0,
                                   cache_len=n_img + t - 1)
         if echo:
           buf = torch.cat([tokens, buf], dim=1)
@@ -189,14 +210,14 @@ class Sampler:
     pos = positions[:, -1].to(torch.int32).contiguous()
     step = torch.zeros(1, dtype=torch.int32, device=dev)
     cur = torch.empty(b, dtype=torch.int32, device=dev)
-    dflags = self._done_flags(b, end_sampling_at_eos_token)
+    dflags = self._done_flags(b, eos_stop)
     self._advance(nxt, buf, step, pos, cur, dflags)
     n_more = steps - 1
     graphable = (self.use_graph and self.greedy_sampling and not return_logits
                  and n_more > 1)
     if graphable:
       done = self._decode_graph(cur, pos, cache, buf, step, n_more,
-                                end_sampling_at_eos_token, events,
+                                eos_stop, events,
                                 cache_len=n_img + t, done_in=dflags)
     else:
       watch = _DoneWatch(dflags)
@@ -236,9 +257,14 @@ class Sampler:
       return None
     return torch.zeros(b + 1, dtype=torch.int32, device=self.device)
 
+  def _eos_args(self):
+    """(eos_id, pad_id, eos_from) of decode_advance: the reference never
+    tests the first token (column 0); per-row stopping does."""
+    return (int(self.vocab.eos_id()), int(self.vocab.pad_id()),
+            0 if self.eos_per_row else 1)
+
   def _advance(self, nxt, buf, step, pos, cur, dflags):
-    ops.ops.decode_advance_(nxt, buf, step, pos, cur, dflags,
-                            int(self.vocab.eos_id()), int(self.vocab.pad_id()))
+    ops.ops.decode_advance_(nxt, buf, step, pos, cur, dflags, *self._eos_args())
 
   def _decode_graph(self, cur, pos, cache, buf, step, n_more, eos_stop,
                     events=None, start=1, cache_len=None, done_in=None):
@@ -255,8 +281,7 @@ class Sampler:
     if eng is None or eng.max_steps < buf.shape[1] or eng.version != version:
       self._graphs.pop(key, None)
       eng = _DecodeGraph(self.model, cache, cur.shape[0], buf.shape[1],
-                         cur.device, eos_stop,
-                         (int(self.vocab.eos_id()), int(self.vocab.pad_id())))
+                         cur.device, eos_stop, self._eos_args())
       eng.version = version
       self._graphs[key] = eng
     return eng.run(cache, cur, pos, buf, step, n_more, events, start,
@@ -343,10 +368,10 @@ class _DecodeGraph:
   """
 
   def __init__(self, model, cache_like, batch, max_steps, device, eos_stop,
-               eos_pad):
+               eos_args):
     self.model = model
     self.max_steps = max_steps
-    self.eos_pad = eos_pad
+    self.eos_args = eos_args
     self.cur = torch.zeros(batch, dtype=torch.int32, device=device)
     self.pos = torch.zeros(batch, dtype=torch.int32, device=device)
     self.buf = torch.zeros(batch, max_steps, dtype=torch.int32, device=device)
@@ -362,12 +387,13 @@ class _DecodeGraph:
       with torch.cuda.graph(self.graph, stream=self.stream):
         self._step()
     torch.cuda.current_stream(device).wait_stream(self.stream)
+    ops.claim_counters(self.stream, self)
 
   def _step(self):
     nxt, _, _ = self.model.next_token(self.cur[:, None], self.pos[:, None],
                                       self.cache, False, inplace=True)
     ops.ops.decode_advance_(nxt, self.buf, self.step, self.pos, self.cur,
-                            self.done, *self.eos_pad)
+                            self.done, *self.eos_args)
 
   @staticmethod
   def _copy_cache(dst_cache, src_cache, slots):

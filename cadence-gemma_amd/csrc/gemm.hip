@@ -988,6 +988,124 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
                nbase, lane, M, N, g);
 }
 
+// 4-wave engine: 256 x 256 x 64 block tile, 4 waves (2 M x 2 N) of one
+// wave per SIMD, wave tile 128 x 128 = 8 x 8 mfma_f32_16x16x32_bf16
+// (256 accumulator registers).  Per K-tile a wave reads 32 KiB of fragments
+// for 128 MFMAs, a third less LDS traffic per MFMA than the 8-wave 128 x 64
+// layout.  Operands go HBM -> LDS by LDS-DMA into two 64 KiB buffers with
+// the same swizzled image as gemm_big_kernel (waves 0-1 move the 256 A rows,
+// waves 2-3 the 256 W rows: 16 pieces of 8 rows x 128 B each).  One barrier
+// per K-tile, placed between the tile's two 32-deep k-steps:
+//   read k-step 1 of tile t | MFMAs k-step 0 | retire reads + DMA of t+1 |
+//   barrier | DMA t+2 into this buffer, read k-step 0 of t+1 | MFMAs k-step 1
+// so every MFMA block starts on fragments already in registers and each
+// DMA has a whole K-tile of MFMAs to land in.
+template <class Epi>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
+    int64_t ldw, int M, int N, int K, int64_t a_goff, int64_t w_goff,
+    Epi epi) {
+  constexpr int BM = 256, TILE = 512 * 8;      // uint4 per K-tile buffer
+  __shared__ __attribute__((aligned(16))) uint4 smem[2 * TILE];
+
+  const int g = blockIdx.y;
+  A += g * a_goff;
+  W += g * w_goff;
+  int m0, n0;
+  big_tile_origin<BM>(M, N, m0, n0);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // DMA sources: wave w moves buffer rows 128 w + 8 i + lane / 8 (i < 16);
+  // lane l of a piece lands at slot l % 8, so it loads source chunk
+  // (l % 8) ^ (l / 8) (the XOR swizzle, an involution)
+  const int src_chunk = (lane & 7) ^ (lane >> 3);
+  const bool isA = wave < 2;
+  const u16* base = isA ? A : W;
+  const int64_t ld = isA ? lda : ldw;
+  const int lim = (isA ? M : N) - 1;
+  const int r0 = (isA ? m0 : n0) + (wave & 1) * 128 + (lane >> 3);
+  uint32_t soff[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    soff[i] = (uint32_t)((int64_t)min(r0 + 8 * i, lim) * ld + src_chunk * 8);
+  auto dma = [&](int buf, int k0) {
+    uint4* dst = &smem[buf * TILE + wave * 16 * 64];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      __builtin_amdgcn_global_load_lds((gptr_t)(base + soff[i] + k0),
+                                       (lptr_t)(dst + i * 64), 16, 0, 0);
+  };
+  const int xr = lane & 7;
+  auto rd = [&](int buf, int ks, bf16x8 (&a)[8], bf16x8 (&b)[8]) {
+    const uint4* s = &smem[buf * TILE];
+    const int ch = (ks * 4 + (lane >> 4)) ^ xr;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      a[i] = __builtin_bit_cast(bf16x8, s[(wm * 128 + i * 16 + (lane & 15)) * 8 + ch]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      b[j] = __builtin_bit_cast(bf16x8,
+                                s[(256 + wn * 128 + j * 16 + (lane & 15)) * 8 + ch]);
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mm = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[8]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0,
+                                                            0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = K / BK;
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  dma(0, 0);
+  if (nk > 1) {
+    dma(1, BK);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  p8_barrier();
+  rd(0, 0, a0, b0);
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    rd(cur, 1, a1, b1);
+    mm(a0, b0);
+    // every read of `cur` retired and this wave's DMA of tile t + 1 landed,
+    // then the barrier publishes both across the workgroup
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(0)" ::: "memory");
+    p8_barrier();
+    if (t + 2 < nk) dma(cur, (t + 2) * BK);
+    if (t + 1 < nk) rd(cur ^ 1, 0, a0, b0);
+    mm(a1, b1);
+  }
+
+  const int mbase = m0 + wm * 128;
+  __syncthreads();   // every wave is done reading the operand buffers
+  u16* st = reinterpret_cast<u16*>(smem) + wave * 2 * (128 * 64);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int nbase = n0 + wn * 128 + h * 64;
+    if (nbase < N) {   // wave-uniform: these columns are not padding
+      f32x4 half[8][4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) half[i][j] = acc[i][h * 4 + j];
+      big_epilogue<Epi, 8>(epi, half, st + h * (128 * 64), mbase, nbase, lane, M, N, g);
+    }
+  }
+}
+
 // Weight-streaming decode GEMM (M <= 32).  One workgroup = NTW x 16 output
 // columns (paired: 16 gate + 16 up packed columns) x one K split; wave w owns
 // k-steps w, w+8, ..., at most KSW of them, and issues ALL of its weight and
@@ -1142,7 +1260,19 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
   if constexpr (!Epi::kPaired && !EpiPairLanes<Epi>::value) {
     if (counters) {
       // in-kernel split-K combine: thread o owns (row o / 16, column o % 16)
-      // of each of the NREP column tiles (MS * 16 <= 512 threads)
+      // of each of the NREP column tiles (MS * 16 <= 512 threads).
+      // Visibility without fences: this is the first measured hand-off row
+      // of MI355X_MICROARCH.md "Workgroup dispatch, XCD placement &
+      // inter-workgroup visibility" -- every slab byte stored `sc1`
+      // (relaxed agent-scope stores, write-through), every storing wave's
+      // `s_waitcnt vmcnt(0)` before the workgroup barrier, ONE lane's agent
+      // atomic add per workgroup on one unsharded counter, and the
+      // workgroup whose add returned S - 1 reading every slab byte with
+      // `sc1` loads (relaxed agent-scope loads, L1 bypass) only after that
+      // add returned and a barrier.  A release / acquire fence pair would
+      // cost ~1.7 us each (same guide, price table) on the critical path of
+      // 51 launches per decode step.
+
       const int o = threadIdx.x, m = o / 16, c = o % 16;
       const bool mine = o < MS * 16 && m < M;
       const int64_t sstride = (int64_t)gridDim.z * M * N;
@@ -1786,6 +1916,8 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
                               splits, parts, packed, st, counters, 0.0f);
 }
 
+int g_engine = 0;   // lab A/B switch of the prefill engine (0 = 8-wave)
+
 // Prefill engine plan for M > kSkinnyMaxM: 0 = 2-buffer 256-row kernel,
 // 160 / 192 / 224 / 256 = 8-phase kernel with that tile height.
 //  * 8-phase when K splits into pairs of 64-deep tiles (an A/B of the
@@ -1895,6 +2027,27 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                          parts, sk, 1, (int)M, (int)N, epi);
       return (int)hipGetLastError();
     }
+    if (g_engine == 1 && K % BK == 0) {
+      // lab switch (cadence_gemm_set_engine): the 4-wave 256 x 256 engine
+      const dim3 wgrid((unsigned)(((M + 255) / 256) * ((N + 255) / 256)), (unsigned)groups);
+      if constexpr (std::is_same_v<Epi, EpiLinear>) {
+#define CADENCE_W4_ACT(ACT_)                                                              \
+  hipLaunchKernelGGL((gemm_w4_kernel<EpiLinearA<ACT_>>), wgrid, dim3(256), 0, st, A, lda, W, \
+                     ldw, (int)M, (int)N, (int)K, a_goff, w_goff, EpiLinearA<ACT_>{epi})
+        switch (epi.act) {
+          case 0: CADENCE_W4_ACT(0); break;
+          case 1: CADENCE_W4_ACT(1); break;
+          case 2: CADENCE_W4_ACT(2); break;
+          case 3: CADENCE_W4_ACT(3); break;
+          default: return (int)hipErrorInvalidValue;
+        }
+#undef CADENCE_W4_ACT
+      } else {
+        hipLaunchKernelGGL((gemm_w4_kernel<Epi>), wgrid, dim3(256), 0, st, A, lda, W, ldw,
+                           (int)M, (int)N, (int)K, a_goff, w_goff, epi);
+      }
+      return (int)hipGetLastError();
+    }
     dim3 grid((unsigned)tiles, (unsigned)groups);
     if constexpr (std::is_same_v<Epi, EpiLinear>) {
 #define CADENCE_BIG_ACT(ACT_)                                                          \
@@ -1990,7 +2143,13 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 11; }
+int cadence_abi_version(void) { return 12; }
+
+int cadence_gemm_set_engine(int engine) {
+  const int prev = g_engine;
+  g_engine = engine;
+  return prev;
+}
 
 int cadence_gemm_big_splits(int64_t M, int64_t N, int64_t K, int64_t groups) {
   if (M <= kSkinnyMaxM || M <= 0) return 1;

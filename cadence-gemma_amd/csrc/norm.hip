@@ -256,16 +256,19 @@ __global__ __launch_bounds__(256) void segment_info_kernel(
 }
 
 // Greedy-decode bookkeeping on device (no host sync per step):
-// out[b, *step] = next[b] (pad once row b has emitted EOS); pos[b] += 1;
-// cur[b] = the token written; done[b] latches on EOS, done[B] = all rows done
-// (read by the host a few steps late, so it never stalls the GPU); ++*step.
+// out[b, *step] = next[b] (pad once row b is done); pos[b] += 1; cur[b] = the
+// token written; done[b] latches when row b emits EOS in a column >= eos_from
+// (1 = the reference's loop: the token sampled from the prompt is never
+// tested, recurrentgemma/torch/sampler.py:177-187,291-300), done[B] = all rows
+// done (read by the host a few steps late, so it never stalls the GPU);
+// ++*step.
 __global__ void decode_advance_kernel(const int32_t* __restrict__ next,
                                       int32_t* __restrict__ out, int64_t ldo,
                                       int32_t* __restrict__ step,
                                       int32_t* __restrict__ pos,
                                       int32_t* __restrict__ cur,
                                       int32_t* __restrict__ done, int eos_id,
-                                      int pad_id, int B) {
+                                      int pad_id, int eos_from, int B) {
   const int b = threadIdx.x;
   const int s = *step;
   int fin = 1;
@@ -274,7 +277,7 @@ __global__ void decode_advance_kernel(const int32_t* __restrict__ next,
     if (done) {
       const int d = done[b];
       if (d) t = pad_id;
-      fin = d | (t == eos_id);
+      fin = d | (t == eos_id && s >= eos_from);
       done[b] = fin;
     }
     out[(int64_t)b * ldo + s] = t;
@@ -295,14 +298,15 @@ extern "C" {
 int cadence_decode_advance(const int32_t* next_token, int32_t* tokens_out,
                            int64_t ld_out, int32_t* step, int32_t* positions,
                            int32_t* cur_out, int32_t* done, int32_t eos_id,
-                           int32_t pad_id, int64_t B, void* stream) {
+                           int32_t pad_id, int32_t eos_from, int64_t B,
+                           void* stream) {
   if (B <= 0) return 0;
   if (B > 1024) return (int)hipErrorInvalidValue;
   const unsigned threads = (unsigned)((B + 63) / 64 * 64);
   hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(threads), 0,
                      static_cast<hipStream_t>(stream), next_token, tokens_out,
                      ld_out, step, positions, cur_out, done, eos_id, pad_id,
-                     (int)B);
+                     (int)eos_from, (int)B);
   return (int)hipGetLastError();
 }
 

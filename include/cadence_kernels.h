@@ -87,6 +87,10 @@ int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups);
  * the epilogue to the split-order sums.  Host-only arithmetic. */
 int cadence_gemm_big_splits(int64_t M, int64_t N, int64_t K, int64_t groups);
 
+/* Lab A/B switch of the prefill engine (0 = 8-wave gemm_big_kernel, 1 =
+ * 4-wave gemm_w4_kernel); returns the previous value.  Host state only. */
+int cadence_gemm_set_engine(int engine);
+
 /* ---- GEMMs with fused epilogues ---------------------------------------- */
 
 /* out[map(m), n] = act(A[m,:] . W[n,:] + bias[n]) (+ resid[map(m), n])
@@ -449,11 +453,14 @@ int cadence_kv_ring_update(const void* k_new, const void* v_new, void* cache_k,
  * row b has emitted eos_id; positions[b] += 1; *step += 1; cur_out[b] = the
  * token written (the next step's input; cur_out may be null).  done (may be
  * null: no EOS handling) is int32[B + 1]: done[b] latches when row b emits
- * eos_id, done[B] = 1 when every row is done.  B <= 1024. */
+ * eos_id into a column >= eos_from (1: the reference loop, which never tests
+ * the token sampled from the prompt; 0: every column), done[B] = 1 when
+ * every row is done.  B <= 1024. */
 int cadence_decode_advance(const int32_t* next_token, int32_t* tokens_out,
                            int64_t ld_out, int32_t* step, int32_t* positions,
                            int32_t* cur_out, int32_t* done, int32_t eos_id,
-                           int32_t pad_id, int64_t B, void* stream);
+                           int32_t pad_id, int32_t eos_from, int64_t B,
+                           void* stream);
 
 #ifdef __cplusplus
 }  // extern "C"

@@ -208,8 +208,10 @@ def cache_from_prompt(keys, values, segment_pos, window):
   return dict(keys=rk, values=rv, num_tokens=num_tokens.to(torch.int32))
 
 
-def local_attention(x, segment_pos, p, prefix, num_heads, window, cache=None):
-  """modules.py:402-483 (MQA: one shared K/V head)."""
+def local_attention(x, segment_pos, p, prefix, num_heads, window, cache=None,
+                    return_cache=True):
+  """modules.py:402-483 (MQA: one shared K/V head); the cache update runs
+  only when return_cache (modules.py:445-451)."""
   b, t, d = x.shape
   hd = d // num_heads
   q = linear(x, p[prefix + "proj_q.weight"]).unflatten(-1, (num_heads, hd))
@@ -223,7 +225,9 @@ def local_attention(x, segment_pos, p, prefix, num_heads, window, cache=None):
     mask = cache_mask(t, cache["num_tokens"], window)
     # modules.py:188-225 (_update_attention_cache): n_fill = min(window, t)
     n_fill = min(window, t)
-    if n_fill == 1:
+    if not return_cache:
+      new_cache = None
+    elif n_fill == 1:
       # single-token decode writes the ring slot in place
       slot = cache["num_tokens"] % window
       nk, nv = cache["keys"].clone(), cache["values"].clone()

@@ -107,6 +107,13 @@ def test_attention_cached_prompt_chunk(dev, hd, num_heads, chunk):
   _cache_close(new, new_ref)
   with pytest.raises(NotImplementedError):   # 1 < t < window (modules.py:224)
     blk(y[:, :3].to(dev), sp[:, :3].to(dev), cache)
+  # without a returned cache the reference never reaches that raise: it
+  # attends over [ring | 3 new rows] with the cache mask (modules.py:439-451)
+  want, none_ref = R.local_attention(y[:, :3], sp[:, :3], p, "", num_heads,
+                                     window, cache_ref, return_cache=False)
+  got, none = blk(y[:, :3].to(dev), sp[:, :3].to(dev), cache, return_cache=False)
+  assert none is None and none_ref is None
+  assert_close_bf16(got, want, **TOL, what="cached 3-token step, no cache")
 
 
 @pytest.mark.parametrize("width", [128, 1024])

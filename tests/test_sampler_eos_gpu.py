@@ -1,10 +1,16 @@
 """Sampler stopping and sampling modes on the GPU.
 
-EOS handling follows the intent of recurrentgemma/torch/sampler.py:177-223
-(`done |= next_token == eos`, loop while any row is not done) with per-row
-flags kept on the device by `decode_advance`: once a row emits EOS the rest
-of its buffer is pad, and the host stops issuing steps once every row is
-done (it reads the flag a few steps late; late steps only write pad).
+Default EOS handling is the reference's loop (recurrentgemma/torch/
+sampler.py:177-187, 209-225, 291-300): `done_now = torch.equal(next_token,
+eos)` with eos a [1] tensor, so a batch of one row stops after a DECODE step
+samples EOS (the token sampled from the prompt, column 0, is never tested;
+the rest of the buffer stays pad) and rows of a larger batch never stop.
+`_reference_loop` below restates that loop on a free run's tokens.
+
+`Sampler(eos_per_row=True)` is the opt-in per-row mode, flags kept on the
+device by `decode_advance`: once a row emits EOS (column 0 included) the
+rest of its buffer is pad, and the host stops issuing steps once every row
+is done (it reads the flag a few steps late; late steps only write pad).
 Categorical sampling (`greedy_sampling=False`, sampler.py:130-136).
 """
 
@@ -23,6 +29,23 @@ class EosVocab(MockVocab):
 
   def eos_id(self):
     return self._eos
+
+
+def _reference_loop(free, eos, pad):
+  """recurrentgemma/torch/sampler.py:209-225 on the free run's tokens: the
+  while loop runs while step < total - 1 and not all(done); done |=
+  torch.equal(next_token [B], eos [1]), which only a 1-row batch can meet."""
+  b, steps = free.shape
+  want = torch.full_like(free, pad)
+  want[:, 0] = free[:, 0]                       # sampled from the prompt
+  done = False
+  step = 0
+  while step < steps - 1 and not done:
+    nxt = free[:, step + 1]
+    want[:, step + 1] = nxt
+    done = done or torch.equal(nxt, torch.tensor([eos], dtype=nxt.dtype))
+    step += 1
+  return want
 
 
 def _expected_with_eos(free, eos, pad):
@@ -48,7 +71,7 @@ def test_eos_stop_pads_rows_and_graph_reuse(dev, use_graph):
       tok, lens, steps).tokens_buffer.cpu() for tok, lens in runs]
   # the most frequent generated token of the first run acts as EOS
   eos = int(torch.mode(free[0].flatten()).values)
-  s = cadence.Sampler(m, EosVocab(eos), use_graph=use_graph)
+  s = cadence.Sampler(m, EosVocab(eos), use_graph=use_graph, eos_per_row=True)
   for (tok, lens), fr in zip(runs, free):
     # same sampler twice (graph and its static buffers reused), stop on EOS
     st = s.generate(tok, lens, steps, end_sampling_at_eos_token=True)
@@ -71,13 +94,48 @@ def test_eos_all_rows_finish_early(dev):
   first = cadence.Sampler(m, MockVocab(), use_graph=False).generate(
       tok, lens, 2).tokens_buffer.cpu()[:, 0]
   assert bool((first == first[0]).all())       # identical rows
-  s = cadence.Sampler(m, EosVocab(int(first[0])), use_graph=True)
+  s = cadence.Sampler(m, EosVocab(int(first[0])), use_graph=True,
+                      eos_per_row=True)
   st = s.generate(tok, lens, 64, end_sampling_at_eos_token=True)
   buf = st.tokens_buffer.cpu()
   assert torch.equal(buf[:, 0], first)
   assert bool((buf[:, 1:] == 0).all())
   assert int(st.step) < 64                     # stopped early
   assert bool(st.done.all())
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_eos_reference_semantics(dev, use_graph):
+  """Default mode = the reference loop: B > 1 never stops or pads; B = 1
+  stops after a decode step emits EOS but not on the first token."""
+  cfg = small_config(vocab=64, window=32)
+  m, _ = make_model(dev, cfg, seed=34)
+  steps = 40
+  g = torch.Generator().manual_seed(5)
+  tok = torch.randint(3, cfg.vocab_size, (3, 13), generator=g, dtype=torch.int32)
+  lens = torch.full((3,), 13, dtype=torch.int32)
+  free = cadence.Sampler(m, MockVocab(), use_graph=False).generate(
+      tok, lens, steps).tokens_buffer.cpu()
+  # an EOS every row emits somewhere after column 0: the batch still runs on
+  eos = int(torch.mode(free[:, 1:].flatten()).values)
+  s = cadence.Sampler(m, EosVocab(eos), use_graph=use_graph)
+  st = s.generate(tok, lens, steps, end_sampling_at_eos_token=True)
+  assert torch.equal(st.tokens_buffer.cpu(), free)
+  assert not bool(st.done.any())
+  # B = 1: each row alone, EOS = a token it emits after column 0
+  for r in range(3):
+    fr = cadence.Sampler(m, MockVocab(), use_graph=False).generate(
+        tok[r:r + 1], lens[:1], steps).tokens_buffer.cpu()
+    e = int(fr[0, steps // 2])
+    s1 = cadence.Sampler(m, EosVocab(e), use_graph=use_graph)
+    st = s1.generate(tok[r:r + 1], lens[:1], steps, end_sampling_at_eos_token=True)
+    assert torch.equal(st.tokens_buffer.cpu(), _reference_loop(fr, e, 0)), (r, e)
+    if r == 0:
+      # the FIRST token as EOS: the reference does not stop on it
+      e0 = int(fr[0, 0])
+      s0 = cadence.Sampler(m, EosVocab(e0), use_graph=use_graph)
+      st = s0.generate(tok[:1], lens[:1], steps, end_sampling_at_eos_token=True)
+      assert torch.equal(st.tokens_buffer.cpu(), _reference_loop(fr, e0, 0))
 
 
 def test_categorical_sampling(dev):
