@@ -41,7 +41,12 @@ namespace {
 constexpr int MODE_LOCAL = 0;
 constexpr int MODE_VIT = 1;
 constexpr int KT = 32;  // keys per tile
-constexpr int kDecodeSplits = 8;  // window splits of the decode attention
+constexpr int kDecodeSplitsMax = 32;  // window ranges of the decode attention
+// ranges per sequence: enough workgroups to cover the CUs at any batch
+inline int decode_splits(int64_t B) {
+  const int64_t ns = 256 / (B > 0 ? B : 1);
+  return (int)(ns < 1 ? 1 : ns > kDecodeSplitsMax ? kDecodeSplitsMax : ns);
+}
 
 struct AttnArgs {
   const u16* q; int64_t q_bs, q_rs, q_hs;   // batch / row / head strides
@@ -286,41 +291,85 @@ struct DecodeArgs {
   int32_t* sems;          // [B] zeroed arrival counters (NS > 1)
 };
 
-// 4 waves per (sequence, window split): all stage the K / V^T tiles, each computes the
-// (cheap) 16 x 32 score tile and softmax redundantly, and each owns a
-// quarter of the head dim in P.V and in the output.
-//
-// Split over the window (gridDim.y = NS): split s takes its share of the
-// non-empty key tiles (the ring tiles below the fill level plus the tile of
-// the new key), keeps its own online-softmax state, and publishes
-// (m, l, unnormalised o) per query row with write-through stores; the last
-// split to arrive at the sequence's counter combines the NS partials in
-// split order (fixed, so replays are bit-identical), writes the output and
-// performs the cache update.  Hand-off: MI355X_MICROARCH "inter-workgroup
-// visibility", first protocol row (sc1 stores and loads, one relaxed agent
-// atomic per workgroup, no fences).
+// Split over the window (gridDim.y = NS): the B x NS workgroups cover the
+// sequence's non-empty keys -- ring slots [0, slot_hi) then the new key,
+// nk = slot_hi + 1 in all -- in NS contiguous ranges of C = ceil(nk / NS)
+// keys rounded up to 16 (ranges past nk exit at once).  A range is streamed
+// in tiles of 64 keys: every K and V byte of the tile is loaded up front into
+// registers (the next tile's loads go out as soon as this one is in LDS), K
+// is stored with the row swizzle of the QK^T fragment reads, V row-major with
+// a 32-B-slot XOR for the transposed P.V reads (ds_read_b64_tr_b16: 4 keys x
+// 16 dims per 16-lane group, two per MFMA B fragment), so no V transpose
+// pass exists.  The 4 waves compute the 16 x 64 score tile redundantly (the
+// query heads are the MFMA rows) and each owns a quarter of the head dim in
+// P.V.  A range keeps its own online-softmax state and, with NS > 1,
+// publishes (m, l, unnormalised o) of the H real heads with write-through
+// stores; the last range to arrive at the sequence's counter combines the
+// partials in range order (fixed, so replays are bit-identical), writes the
+// output and performs the cache update.  Hand-off: MI355X_MICROARCH
+// "inter-workgroup visibility", first protocol row (sc1 stores and loads,
+// one relaxed agent atomic per workgroup, no fences).
+constexpr int kDecodeKT = 64;   // keys per tile
+
+// V image slot XOR: rows {0..3, 8..11} (and {4..7, 12..15}) of a 16-row
+// block land on distinct 32-B slots of a 256-B bank row, so each
+// ds_read_b64_tr_b16 (one 32-lane half = two 4-row blocks 8 rows apart) is
+// conflict-free; a multiple of 2 keeps a row's two 16-B chunks of one 32-B
+// slot together.
+template <int CPR>
+CADENCE_DEV int vswz(int row) {
+  return CPR >= 16 ? 2 * ((row & 3) | (((row >> 3) & 1) << 2)) : 2 * (row & 3);
+}
+
 template <int HD>
 __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
-  constexpr int KS = HD / 32, NO = HD / 16 / 4, CPR = HD / 8;
-  __shared__ uint4 ks_[KT * HD / 8];
-  __shared__ u16 vt[HD * KT];
+  constexpr int KS = HD / 32, NO = HD / 64, CPR = HD / 8;
+  constexpr int KT = kDecodeKT, LPT = KT * CPR / 256;   // 16-B loads per operand
+  __shared__ uint4 ks_[KT * CPR];
+  __shared__ uint4 vs_[KT * CPR];
   __shared__ u16 ptall[4][16 * KT];
   __shared__ int ticket;
   __shared__ __attribute__((aligned(16))) float ml[32];   // split m[16], l[16]
+  __shared__ float mls[kDecodeSplitsMax * 32];            // combine: all ranges'
   const int b = blockIdx.x;
   const int split = blockIdx.y, NS = gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   u16* pt = ptall[wave];
-  const int dbase = wave * NO * 16;
+  const int dbase = wave * (HD / 4);
   const int nt = a.num_tokens[b];
   const int qpos = nt;
   const int kblk = nt / a.W;
-  const int nslots = a.W + 1;  // ring slots + the new key
   // slots with a non-negative position: all of them once the ring wrapped
   const int slot_hi = nt >= a.W ? a.W : nt;
+  const int nk = slot_hi + 1;                   // + the new key
+  const int C = (((nk + NS - 1) / NS) + 15) & ~15;
+  const int nsp = (nk + C - 1) / C;             // active ranges
+  if (split >= nsp) return;
+  const int kb = split * C, ke = min(nk, kb + C);
 
-  // branch-free loads throughout (absent rows / slots read the zero page)
+  // branch-free loads throughout (absent rows / keys read the zero page)
   const u16* zpage = reinterpret_cast<const u16*>(kZeroPage + lane);
+  const u16* ckb = a.ck + (int64_t)b * a.W * a.hd;
+  const u16* cvb = a.cv + (int64_t)b * a.W * a.hd;
+  const u16* knb = a.k_new + (int64_t)b * a.new_rs;
+  const u16* vnb = a.v_new + (int64_t)b * a.new_rs;
+  // the cache update's rows, loaded now so the update at the end waits for
+  // nothing
+  const uint4 knew = ld16(knb + min(tid * 8, HD - 8));
+  const uint4 vnew = ld16(vnb + min(tid * 8, HD - 8));
+  uint4 kreg[LPT], vreg[LPT];
+  auto fetch = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + i * 256;
+      const int j = t0 + c / CPR, d = (c % CPR) * 8;
+      const bool ring = j < slot_hi, fresh = j == slot_hi && j < ke;
+      const int64_t roff = (int64_t)j * a.hd + d;
+      kreg[i] = ld16(ring && j < ke ? ckb + roff : fresh ? knb + d : zpage);
+      vreg[i] = ld16(ring && j < ke ? cvb + roff : fresh ? vnb + d : zpage);
+    }
+  };
+  fetch(kb);
   bf16x8 qf[KS];
   {
     const int hrow = lane & 15;
@@ -340,60 +389,27 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
     m_run[r] = -INFINITY;
     l_run[r] = 0.0f;
   }
-  const u16* ckb = a.ck + (int64_t)b * a.W * a.hd;
-  const u16* cvb = a.cv + (int64_t)b * a.W * a.hd;
-
-  // non-empty tiles: ring tiles below slot_hi, then the tile of slot W
-  const int ring_tiles = (slot_hi + KT - 1) / KT;
-  const int last_tile = a.W / KT;
-  const int ntot = last_tile < ring_tiles ? ring_tiles : ring_tiles + 1;
-  // tiles spread evenly over the splits (graph-timed at B = 32, ctx 320:
-  // 21.3 us; forcing >= 4 tiles per split -- fewer, longer splits -- took
-  // 31.1 us, >= 2 took 21.5); splits past the active ones exit before
-  // touching anything, a single active split writes the output directly
-  const int tps = (ntot + NS - 1) / NS;
-  const int nsp = (ntot + tps - 1) / tps;       // active splits
-  if (split >= nsp) return;
-  const int tb = split * tps, te = min(ntot, tb + tps);
-  (void)nslots;
-  // K / V chunks of a tile in registers; tile ti+1 is fetched while tile ti
-  // is computed (one memory latency per split instead of one per tile)
-  constexpr int CH = KT * CPR / 256;
-  uint4 kreg[CH], vreg[CH];
-  auto fetch = [&](int ti) {
-    const int k0 = (ti < ring_tiles ? ti : last_tile) * KT;
+  const uint32_t vlds = (uint32_t)(uintptr_t)vs_;
+  // transposed-read addresses: lane 4q+p of a 16-lane group reads key row
+  // q of its 4-row block, dims 4p..4p+3 of the 16-dim column block
+  const int tq = (lane & 15) >> 2, tp = lane & 3, g = lane >> 4;
+  for (int t0 = kb; t0 < ke; t0 += KT) {
+    __syncthreads();   // the previous tile's LDS reads are done
 #pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int c = tid + i * 256;
-      const int kr = c / CPR, d = (c % CPR) * 8;
-      const int slot = k0 + kr;
-      const u16* kp = slot < a.W ? ckb + (int64_t)slot * a.hd + d
-                    : slot == a.W ? a.k_new + (int64_t)b * a.new_rs + d : zpage;
-      const u16* vp = slot < a.W ? cvb + (int64_t)slot * a.hd + d
-                    : slot == a.W ? a.v_new + (int64_t)b * a.new_rs + d : zpage;
-      kreg[i] = ld16(kp);
-      vreg[i] = ld16(vp);
-    }
-  };
-  if (tb < te) fetch(tb);
-  for (int ti = tb; ti < te; ++ti) {
-    const int k0 = (ti < ring_tiles ? ti : last_tile) * KT;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
+    for (int i = 0; i < LPT; ++i) {
       const int c = tid + i * 256;
       const int kr = c / CPR, ch = c % CPR;
-      const int d = ch * 8;
       ks_[kr * CPR + swz<CPR>(ch, kr)] = kreg[i];
-      const u16* vs = reinterpret_cast<const u16*>(&vreg[i]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) vt[(d + j) * KT + kr] = vs[j];
+      vs_[kr * CPR + (ch ^ vswz<CPR>(kr))] = vreg[i];
     }
     __syncthreads();
-    if (ti + 1 < te) fetch(ti + 1);
-    f32x4 s[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if (t0 + KT < ke) fetch(t0 + KT);
+    const int nblk = min(4, (ke - t0 + 15) / 16);   // live 16-key blocks
+    f32x4 s[4];
 #pragma unroll
-    for (int jn = 0; jn < 2; ++jn) {
+    for (int jn = 0; jn < 4; ++jn) {
+      s[jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (jn >= nblk) continue;
       const int kr = jn * 16 + (lane & 15);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -402,22 +418,22 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
         s[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, s[jn], 0, 0, 0);
       }
     }
-    float p[2][4], tmax[4];
+    float p[4][4], tmax[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) tmax[r] = -INFINITY;
 #pragma unroll
-    for (int jn = 0; jn < 2; ++jn) {
-      const int slot = k0 + jn * 16 + (lane & 15);
-      // _compute_cache_mask: slot positions from num_tokens
+    for (int jn = 0; jn < 4; ++jn) {
+      const int j = t0 + jn * 16 + (lane & 15);
+      // _compute_cache_mask: slot positions from num_tokens; j == slot_hi
+      // is the new key at the query's own position
       int kpos;
-      if (slot < a.W) {
-        const int now = slot + kblk * a.W;
-        kpos = now < nt ? now : slot + (kblk - 1) * a.W;
+      if (j < slot_hi) {
+        const int now = j + kblk * a.W;
+        kpos = now < nt ? now : j + (kblk - 1) * a.W;
       } else {
         kpos = qpos;
       }
-      const bool ok = slot <= a.W && kpos >= 0 && qpos >= kpos &&
-                      qpos <= kpos + a.W;
+      const bool ok = j < ke && kpos >= 0 && qpos >= kpos && qpos <= kpos + a.W;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float v = ok ? rbf(s[jn][r]) * a.scale : -INFINITY;
@@ -435,7 +451,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
       alpha[r] = (mn == -INFINITY) ? 1.0f : expf(m_run[r] - mn);
       float rs = 0.0f;
 #pragma unroll
-      for (int jn = 0; jn < 2; ++jn) {
+      for (int jn = 0; jn < 4; ++jn) {
         const float e = (mn == -INFINITY) ? 0.0f : expf(p[jn][r] - mn);
         p[jn][r] = e;
         rs += e;
@@ -450,20 +466,38 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[j][r] *= alpha[r];
 #pragma unroll
-    for (int jn = 0; jn < 2; ++jn)
+    for (int jn = 0; jn < 4; ++jn)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         pt[(4 * (lane >> 4) + r) * KT + jn * 16 + (lane & 15)] = f2bf(p[jn][r]);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    const bf16x8 pf = __builtin_bit_cast(
-        bf16x8, *reinterpret_cast<const uint4*>(pt + (lane & 15) * KT + 8 * (lane >> 4)));
+    // O += P . V over each live 32-key half: P fragment (head row, keys
+    // 32 kk + 8 g ..), V^T fragment by two transposed reads (keys 32 kk +
+    // 8 g + {0..3} and {4..7}, dims of this wave's column block)
 #pragma unroll
-    for (int j = 0; j < NO; ++j) {
-      const bf16x8 vf = __builtin_bit_cast(
-          bf16x8, *reinterpret_cast<const uint4*>(
-                      &vt[(dbase + j * 16 + (lane & 15)) * KT + 8 * (lane >> 4)]));
-      o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[j], 0, 0, 0);
+    for (int kk = 0; kk < 2; ++kk) {
+      if (kk * 32 >= nblk * 16) continue;
+      const bf16x8 pf = __builtin_bit_cast(
+          bf16x8, *reinterpret_cast<const uint4*>(pt + (lane & 15) * KT + kk * 32 + 8 * g));
+      const int r1 = kk * 32 + 8 * g + tq, r2 = r1 + 4;
+#pragma unroll
+      for (int j = 0; j < NO; ++j) {
+        const int ch = (dbase + j * 16) / 8 + (tp >> 1);
+        const uint32_t a1 = vlds + (r1 * CPR + (ch ^ vswz<CPR>(r1))) * 16 + 8 * (tp & 1);
+        const uint32_t a2 = vlds + (r2 * CPR + (ch ^ vswz<CPR>(r2))) * 16 + 8 * (tp & 1);
+        uint2 w1, w2;
+        asm volatile(
+            "ds_read_b64_tr_b16 %0, %2\n"
+            "ds_read_b64_tr_b16 %1, %3\n"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(w1), "=&v"(w2)
+            : "v"(a1), "v"(a2)
+            : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(w1.x, w1.y, w2.x, w2.y));
+        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[j], 0, 0, 0);
+      }
     }
   }
   if (nsp == 1) {
@@ -481,28 +515,25 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
   } else {
     constexpr int PS = 32 + 16 * HD;            // floats per split partial
     float* part = a.parts + ((int64_t)b * NS + split) * PS;
-    float* stage = reinterpret_cast<float*>(ks_);   // [16][HD] fp32 = sizeof(ks_)
+    float* stage = reinterpret_cast<float*>(ks_);   // [16][HD] fp32 <= sizeof(ks_)
     __syncthreads();
-    if (tb < te) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int hrow = 4 * (lane >> 4) + r;
+    for (int r = 0; r < 4; ++r) {
+      const int hrow = 4 * (lane >> 4) + r;
 #pragma unroll
-        for (int j = 0; j < NO; ++j)
-          stage[hrow * HD + dbase + j * 16 + (lane & 15)] = o[j][r];
-        if (wave == 0 && (lane & 15) == 0) {
-          ml[hrow] = m_run[r];
-          ml[16 + hrow] = l_run[r];
-        }
+      for (int j = 0; j < NO; ++j)
+        stage[hrow * HD + dbase + j * 16 + (lane & 15)] = o[j][r];
+      if (wave == 0 && (lane & 15) == 0) {
+        ml[hrow] = m_run[r];
+        ml[16 + hrow] = l_run[r];
       }
     }
     __syncthreads();
-    if (tb < te) {
-      for (int q = tid * 4; q < PS; q += 1024) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(q < 32 ? ml + q : stage + (q - 32));
-        float* dst = part + q;
-        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(dst), "v"(v) : "memory");
-      }
+    // m, l of all 16 rows, o of the H real head rows
+    for (int q = tid * 4; q < 32 + a.H * HD; q += 1024) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(q < 32 ? ml + q : stage + (q - 32));
+      float* dst = part + q;
+      asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(dst), "v"(v) : "memory");
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -512,52 +543,63 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
     __syncthreads();
     if (ticket != nsp - 1) return;
     const float* pb = a.parts + (int64_t)b * NS * PS;
-    // every load of the combine is issued before the first use (fixed trip
-    // counts, splits >= nsp predicated off): one memory round trip instead
-    // of one per (row chunk, split)
-    constexpr int QI = 16 * HD / 1024;          // row chunks per thread
-    float ms[QI][kDecodeSplits], ls[QI][kDecodeSplits];
-    uint64_t w0[QI][kDecodeSplits], w1[QI][kDecodeSplits];
+    // One memory round trip for up to 8 ranges: every range's (m, l) rows go
+    // through LDS (one load per thread), and each thread's float4 chunks of
+    // the H x HD output (up to HD / 64 per thread) of all 8
+    // ranges are loaded with 16-B write-through-side (sc1) loads before the
+    // first use; ranges past 8 (only B <= 16) take another trip per 8.
+    constexpr int GS = 8, QP = HD / 64;   // QP x 256 float4 >= 16 heads x HD
+    const int nq = a.H * HD / 4;
+    float mx[QP], l[QP];
+    f32x4 acc[QP];
 #pragma unroll
-    for (int it = 0; it < QI; ++it) {
-      const int q = tid * 4 + it * 1024;
-      const int hrow = q / HD;
+    for (int p = 0; p < QP; ++p) {
+      mx[p] = -INFINITY;
+      l[p] = 0.0f;
+      acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int idx = tid; idx < nsp * 32; idx += 256)
+      mls[idx] = __hip_atomic_load(pb + (idx >> 5) * PS + (idx & 31), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    for (int s0 = 0; s0 < nsp; s0 += GS) {
+      f32x4 w[QP][GS];
 #pragma unroll
-      for (int sp = 0; sp < kDecodeSplits; ++sp) {
-        const bool on = sp < nsp && hrow < a.H;
-        const float* base = pb + (on ? sp : 0) * PS;
-        ms[it][sp] = __hip_atomic_load(base + hrow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ls[it][sp] = __hip_atomic_load(base + 16 + hrow, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(base + 32 + q);
-        w0[it][sp] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        w1[it][sp] = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int p = 0; p < QP; ++p)
+#pragma unroll
+        for (int u = 0; u < GS; ++u) {
+          const int c = min(tid + 256 * p, nq - 1);
+          const float* src = pb + min(s0 + u, nsp - 1) * PS + 32 + 4 * c;
+          asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(w[p][u]) : "v"(src)
+                       : "memory");
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // the (m, l) rows are in LDS
+#pragma unroll
+      for (int p = 0; p < QP; ++p) {
+        const int hrow = min(tid + 256 * p, nq - 1) * 4 / HD;
+#pragma unroll
+        for (int u = 0; u < GS; ++u) {
+          if (s0 + u >= nsp) continue;
+          // running rescale in range order
+          const float mu = mls[(s0 + u) * 32 + hrow], lu = mls[(s0 + u) * 32 + 16 + hrow];
+          const float mn = fmaxf(mx[p], mu);
+          const float sa = mx[p] == -INFINITY ? 0.0f : expf(mx[p] - mn);
+          const float sb = mu == -INFINITY ? 0.0f : expf(mu - mn);
+          l[p] = l[p] * sa + lu * sb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[p][e] = acc[p][e] * sa + w[p][u][e] * sb;
+          mx[p] = mn;
+        }
       }
     }
 #pragma unroll
-    for (int it = 0; it < QI; ++it) {
-      const int q = tid * 4 + it * 1024;
-      const int hrow = q / HD;
-      if (hrow >= a.H) continue;
-      float mx = -INFINITY;
-#pragma unroll
-      for (int sp = 0; sp < kDecodeSplits; ++sp)
-        if (sp < nsp) mx = fmaxf(mx, ms[it][sp]);
-      float l = 0.0f, acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int sp = 0; sp < kDecodeSplits; ++sp) {
-        if (sp >= nsp) continue;
-        const float wgt = (ms[it][sp] == -INFINITY) ? 0.0f : expf(ms[it][sp] - mx);
-        l += ls[it][sp] * wgt;
-        acc[0] += __uint_as_float((uint32_t)w0[it][sp]) * wgt;
-        acc[1] += __uint_as_float((uint32_t)(w0[it][sp] >> 32)) * wgt;
-        acc[2] += __uint_as_float((uint32_t)w1[it][sp]) * wgt;
-        acc[3] += __uint_as_float((uint32_t)(w1[it][sp] >> 32)) * wgt;
-      }
-      const float inv = l > 0.0f ? 1.0f / l : 0.0f;
-      u16* dst = a.o + xoff(b, q, a.ldo, a.omt);
-      const uint32_t lo = (uint32_t)f2bf(acc[0] * inv) | ((uint32_t)f2bf(acc[1] * inv) << 16);
-      const uint32_t hi = (uint32_t)f2bf(acc[2] * inv) | ((uint32_t)f2bf(acc[3] * inv) << 16);
+    for (int p = 0; p < QP; ++p) {
+      const int c = tid + 256 * p;
+      if (c >= nq) continue;
+      const float inv = l[p] > 0.0f ? 1.0f / l[p] : 0.0f;
+      u16* dst = a.o + xoff(b, 4 * c, a.ldo, a.omt);
+      const uint32_t lo = (uint32_t)f2bf(acc[p][0] * inv) | ((uint32_t)f2bf(acc[p][1] * inv) << 16);
+      const uint32_t hi = (uint32_t)f2bf(acc[p][2] * inv) | ((uint32_t)f2bf(acc[p][3] * inv) << 16);
       *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
     }
     if (tid == 0)
@@ -565,14 +607,12 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
   }
   // _update_attention_cache: write the new key/value into slot nt % W, then
   // bump num_tokens (all reads of this sequence's cache are done: with NS > 1
-  // every split has arrived before the last one gets here).
+  // every range has arrived before the last one gets here).
   __syncthreads();
   const int slot = nt % a.W;
-  for (int d = tid * 8; d < a.hd; d += 2048) {
-    st16(a.ck + ((int64_t)b * a.W + slot) * a.hd + d,
-         ld16(a.k_new + (int64_t)b * a.new_rs + d));
-    st16(a.cv + ((int64_t)b * a.W + slot) * a.hd + d,
-         ld16(a.v_new + (int64_t)b * a.new_rs + d));
+  if (tid * 8 < HD) {
+    st16(a.ck + ((int64_t)b * a.W + slot) * a.hd + tid * 8, knew);
+    st16(a.cv + ((int64_t)b * a.W + slot) * a.hd + tid * 8, vnew);
   }
   if (tid == 0) a.num_tokens[b] = nt + 1;
 }
@@ -803,7 +843,7 @@ int cadence_kv_cache_fill(const void* k, const void* v,
 }
 
 int64_t cadence_local_attention_decode_workspace_bytes(int64_t B, int64_t hd) {
-  return B * kDecodeSplits * (32 + 16 * hd) * 4;
+  return B * decode_splits(B) * (32 + 16 * hd) * 4;
 }
 
 int cadence_local_attention_decode(const void* q, const void* k_new,
@@ -827,7 +867,7 @@ int cadence_local_attention_decode(const void* q, const void* k_new,
                (int)window, 1.0f / sqrtf((float)hd),
                static_cast<float*>(workspace), sems};
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const dim3 grid((unsigned)B, split ? kDecodeSplits : 1);
+  const dim3 grid((unsigned)B, split ? decode_splits(B) : 1);
   if (hd == 256)
     hipLaunchKernelGGL(decode_attn_kernel<256>, grid, dim3(256), 0, st, a);
   else if (hd == 128)

@@ -1000,12 +1000,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(
 //   barrier | DMA t+2 into this buffer, read k-step 0 of t+1 | MFMAs k-step 1
 // so every MFMA block starts on fragments already in registers and each
 // DMA has a whole K-tile of MFMAs to land in.
-template <class Epi>
+template <class Epi, int MR>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
     int64_t ldw, int M, int N, int K, int64_t a_goff, int64_t w_goff,
     Epi epi) {
-  constexpr int BM = 256, TILE = 512 * 8;      // uint4 per K-tile buffer
+  constexpr int BM = 32 * MR, TILE = 512 * 8;  // uint4 per K-tile buffer
   __shared__ __attribute__((aligned(16))) uint4 smem[2 * TILE];
 
   const int g = blockIdx.y;
@@ -1024,49 +1024,90 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
   const bool isA = wave < 2;
   const u16* base = isA ? A : W;
   const int64_t ld = isA ? lda : ldw;
-  const int lim = (isA ? M : N) - 1;
-  const int r0 = (isA ? m0 : n0) + (wave & 1) * 128 + (lane >> 3);
+  // A halves hold 16 MR rows (pieces past them re-load the half's last row)
+  const int half0 = (isA ? m0 + (wave & 1) * 16 * MR : n0 + (wave & 1) * 128);
+  const int hlim = min((isA ? M : N) - 1, half0 + (isA ? 16 * MR : 128) - 1);
+  // 32-bit byte offsets from a wave-uniform base: saddr + voffset loads,
+  // no 64-bit address arithmetic per piece
   uint32_t soff[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i)
-    soff[i] = (uint32_t)((int64_t)min(r0 + 8 * i, lim) * ld + src_chunk * 8);
+    soff[i] = (uint32_t)(((int64_t)min(half0 + 8 * i + (lane >> 3), hlim) * ld +
+                          src_chunk * 8) * 2);
   auto dma = [&](int buf, int k0) {
     uint4* dst = &smem[buf * TILE + wave * 16 * 64];
+    const char* bk = reinterpret_cast<const char*>(base + k0);
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      __builtin_amdgcn_global_load_lds((gptr_t)(base + soff[i] + k0),
-                                       (lptr_t)(dst + i * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gptr_t)(bk + soff[i]), (lptr_t)(dst + i * 64), 16,
+                                       0, 0);
   };
   const int xr = lane & 7;
-  auto rd = [&](int buf, int ks, bf16x8 (&a)[8], bf16x8 (&b)[8]) {
-    const uint4* s = &smem[buf * TILE];
+  // fragment read r of a k-step: r < MR = A row block r, else B column block
+  // r - MR (ds_read_b128, XOR-swizzled chunk)
+  auto rd1 = [&](int buf, int ks, int r, bf16x8& f) {
+    const uint4* sp = &smem[buf * TILE];
     const int ch = (ks * 4 + (lane >> 4)) ^ xr;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      a[i] = __builtin_bit_cast(bf16x8, s[(wm * 128 + i * 16 + (lane & 15)) * 8 + ch]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      b[j] = __builtin_bit_cast(bf16x8,
-                                s[(256 + wn * 128 + j * 16 + (lane & 15)) * 8 + ch]);
+    const int row = r < MR ? wm * 128 + r * 16 : 256 + wn * 128 + (r - MR) * 16;
+    f = __builtin_bit_cast(bf16x8, sp[(row + (lane & 15)) * 8 + ch]);
   };
-  f32x4 acc[8][8];
+  f32x4 acc[MR][8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MR; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mm = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[8]) {
-    __builtin_amdgcn_s_setprio(1);
+  // One segment = the MR x 8 MFMAs of one 32-deep k-step, with the next
+  // k-step's MR + 8 fragment reads (after MFMAs 0, 3, 6, ...) and, when
+  // `dma`, the 16 LDS-DMA pieces of a later K-tile (after MFMAs 1, 4, ...)
+  // threaded between them.  The MFMAs are inline asm tied to their AGPR
+  // accumulators ("+a"): with the builtin, hipcc re-allocates some
+  // accumulators every iteration of this 224-256-accumulator loop and
+  // shuffles them through v_accvgpr_mov / VGPR copies; an asm statement with
+  // side effects also keeps the interleave in source order.  (hipcc inserts
+  // no wait states for asm MFMAs: the loop's operands are only ds_read /
+  // MFMA results, and the epilogue below waits explicitly.)
+  const int nk = K / BK;
+  // past the last K-tile the DMA pieces read the zero page (lane-linear
+  // 16 B each) instead of branching around them
+  const uint32_t zoff = lane * 16;
+  const char* zpage = reinterpret_cast<const char*>(kZeroPage);
+  auto segment = [&](const bf16x8 (&a)[MR], const bf16x8 (&b)[8], bf16x8 (&na)[MR],
+                     bf16x8 (&nb)[8], int rbuf, int rks, bool dma_on, int dbuf,
+                     int dtile) {
+    uint4* dst = &smem[dbuf * TILE + wave * 16 * 64];
+    const bool live = dtile < nk;
+    const char* bk = live ? reinterpret_cast<const char*>(base + dtile * BK) : zpage;
+    int nr = 0, nd = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int n = 0; n < MR * 8; ++n) {
+      const int i = n / 8, j = n % 8;
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                   : "+a"(acc[i][j]) : "v"(a[i]), "v"(b[j]));
+      if (n % 3 == 0 && nr < MR + 8) {
+        if (nr < MR) rd1(rbuf, rks, nr, na[nr]);
+        else rd1(rbuf, rks, nr, nb[nr - MR]);
+        ++nr;
+      }
+      if (dma_on && n % 3 == 1 && nd < 16) {
+        __builtin_amdgcn_global_load_lds((gptr_t)(bk + (live ? soff[nd] : zoff)),
+                                         (lptr_t)(dst + nd * 64), 16, 0, 0);
+        ++nd;
+      }
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0,
-                                                            0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    for (; nr < MR + 8; ++nr) {
+      if (nr < MR) rd1(rbuf, rks, nr, na[nr]);
+      else rd1(rbuf, rks, nr, nb[nr - MR]);
+    }
+#pragma unroll
+    for (; nd < 16; ++nd) {
+      if (!dma_on) break;
+      __builtin_amdgcn_global_load_lds((gptr_t)(bk + (live ? soff[nd] : zoff)),
+                                       (lptr_t)(dst + nd * 64), 16, 0, 0);
+    }
   };
 
-  const int nk = K / BK;
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  bf16x8 a0[MR], b0[8], a1[MR], b1[8];
   dma(0, 0);
   if (nk > 1) {
     dma(1, BK);
@@ -1075,33 +1116,45 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   p8_barrier();
-  rd(0, 0, a0, b0);
+#pragma unroll
+  for (int r = 0; r < MR; ++r) rd1(0, 0, r, a0[r]);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) rd1(0, 0, MR + r, b0[r]);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 4" ::: "memory");
+  // K-tile t: segment A = MFMAs of k-step 0 with the reads of k-step 1;
+  // every read of `cur` retired and this wave's DMA of tile t + 1 landed,
+  // then the barrier publishes both; segment B = MFMAs of k-step 1 with
+  // tile t + 2's DMA into the buffer just released and the reads of k-step
+  // 0 of tile t + 1 (past the end: zero-page DMA and reads of dead data,
+  // so the loop stays one branch-free body and hipcc keeps every
+  // accumulator in one AGPR quad throughout -- a peeled tail made it copy
+  // them at the loop exit, reading asm-MFMA results it cannot see pending).
   for (int t = 0; t < nk; ++t) {
     const int cur = t & 1;
-    rd(cur, 1, a1, b1);
-    mm(a0, b0);
-    // every read of `cur` retired and this wave's DMA of tile t + 1 landed,
-    // then the barrier publishes both across the workgroup
+    segment(a0, b0, a1, b1, cur, 1, false, 0, 0);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(0)" ::: "memory");
     p8_barrier();
-    if (t + 2 < nk) dma(cur, (t + 2) * BK);
-    if (t + 1 < nk) rd(cur ^ 1, 0, a0, b0);
-    mm(a1, b1);
+    segment(a1, b1, a0, b0, cur ^ 1, 0, true, cur, t + 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  // the zero-page DMA of the last tile lands before the epilogue reuses the
+  // LDS, and the last asm MFMAs' results before the epilogue reads them
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15"
+               ::: "memory");
 
-  const int mbase = m0 + wm * 128;
+  const int mbase = m0 + wm * 16 * MR;
   __syncthreads();   // every wave is done reading the operand buffers
   u16* st = reinterpret_cast<u16*>(smem) + wave * 2 * (128 * 64);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int nbase = n0 + wn * 128 + h * 64;
     if (nbase < N) {   // wave-uniform: these columns are not padding
-      f32x4 half[8][4];
+      f32x4 half[MR][4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < MR; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) half[i][j] = acc[i][h * 4 + j];
-      big_epilogue<Epi, 8>(epi, half, st + h * (128 * 64), mbase, nbase, lane, M, N, g);
+      big_epilogue<Epi, MR>(epi, half, st + h * (128 * 64), mbase, nbase, lane, M, N, g);
     }
   }
 }
@@ -1916,7 +1969,7 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
                               splits, parts, packed, st, counters, 0.0f);
 }
 
-int g_engine = 0;   // lab A/B switch of the prefill engine (0 = 8-wave)
+int g_engine = 1;   // lab A/B switch of the prefill engine (0 = 8-wave only)
 
 // Prefill engine plan for M > kSkinnyMaxM: 0 = 2-buffer 256-row kernel,
 // 160 / 192 / 224 / 256 = 8-phase kernel with that tile height.
@@ -2027,13 +2080,22 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                          parts, sk, 1, (int)M, (int)N, epi);
       return (int)hipGetLastError();
     }
-    if (g_engine == 1 && K % BK == 0) {
-      // lab switch (cadence_gemm_set_engine): the 4-wave 256 x 256 engine
-      const dim3 wgrid((unsigned)(((M + 255) / 256) * ((N + 255) / 256)), (unsigned)groups);
+    // long-K GEMMs whose tile plan is 224 or 256 rows run on the 4-wave
+    // engine (its MFMA loop is 6-9 % faster there); short K keeps the 8-wave
+    // engine, whose 8 waves finish the element-wise epilogues twice as fast
+    if (g_engine != 0 && K >= 2048 && (rows == 224 || rows == 256)) {
+      const dim3 wgrid((unsigned)(((M + rows - 1) / rows) * ((N + 255) / 256)),
+                       (unsigned)groups);
       if constexpr (std::is_same_v<Epi, EpiLinear>) {
 #define CADENCE_W4_ACT(ACT_)                                                              \
-  hipLaunchKernelGGL((gemm_w4_kernel<EpiLinearA<ACT_>>), wgrid, dim3(256), 0, st, A, lda, W, \
-                     ldw, (int)M, (int)N, (int)K, a_goff, w_goff, EpiLinearA<ACT_>{epi})
+  if (rows == 224)                                                                        \
+    hipLaunchKernelGGL((gemm_w4_kernel<EpiLinearA<ACT_>, 7>), wgrid, dim3(256), 0, st, A,   \
+                       lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff,               \
+                       EpiLinearA<ACT_>{epi});                                            \
+  else                                                                                    \
+    hipLaunchKernelGGL((gemm_w4_kernel<EpiLinearA<ACT_>, 8>), wgrid, dim3(256), 0, st, A,   \
+                       lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff,               \
+                       EpiLinearA<ACT_>{epi})
         switch (epi.act) {
           case 0: CADENCE_W4_ACT(0); break;
           case 1: CADENCE_W4_ACT(1); break;
@@ -2042,8 +2104,11 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
           default: return (int)hipErrorInvalidValue;
         }
 #undef CADENCE_W4_ACT
+      } else if (rows == 224) {
+        hipLaunchKernelGGL((gemm_w4_kernel<Epi, 7>), wgrid, dim3(256), 0, st, A, lda, W, ldw,
+                           (int)M, (int)N, (int)K, a_goff, w_goff, epi);
       } else {
-        hipLaunchKernelGGL((gemm_w4_kernel<Epi>), wgrid, dim3(256), 0, st, A, lda, W, ldw,
+        hipLaunchKernelGGL((gemm_w4_kernel<Epi, 8>), wgrid, dim3(256), 0, st, A, lda, W, ldw,
                            (int)M, (int)N, (int)K, a_goff, w_goff, epi);
       }
       return (int)hipGetLastError();

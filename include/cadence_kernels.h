@@ -87,8 +87,10 @@ int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups);
  * the epilogue to the split-order sums.  Host-only arithmetic. */
 int cadence_gemm_big_splits(int64_t M, int64_t N, int64_t K, int64_t groups);
 
-/* Lab A/B switch of the prefill engine (0 = 8-wave gemm_big_kernel, 1 =
- * 4-wave gemm_w4_kernel); returns the previous value.  Host state only. */
+/* Lab A/B switch of the prefill engine: 1 (default) = the shipped plan (the
+ * 4-wave gemm_w4_kernel for K >= 2048 on 224 / 256-row tile plans, else the
+ * 8-wave gemm_big_kernel), 0 = 8-wave only; returns the previous value.
+ * Host state only. */
 int cadence_gemm_set_engine(int engine);
 
 /* ---- GEMMs with fused epilogues ---------------------------------------- */

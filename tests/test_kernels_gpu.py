@@ -396,6 +396,46 @@ def test_rope_and_local_attention(dev, b, t, h, hd, window, split):
   assert rel_l2(got, want) < 1e-2
 
 
+@pytest.mark.parametrize("b,ctx", [(32, 352), (1, 1500), (2, 2100), (4, 0)])
+def test_decode_attention_ranges(dev, b, ctx):
+  """Decode attention at the bench batch (8 key ranges per sequence, one
+  tile each), a single sequence (32 ranges: the combine's second group), a
+  wrapped 2048-slot ring (several 64-key tiles per range) and an empty
+  cache (only the new key), against the reference's cache mask
+  (modules.py:155-185) and ring update (modules.py:206-218)."""
+  g = torch.Generator().manual_seed(20 + b)
+  h, hd, window = 10, 256, 2048
+  ck = rnd(b, window, 1, hd, gen=g)
+  cv = rnd(b, window, 1, hd, gen=g)
+  nt = torch.tensor([ctx + 3 * i for i in range(b)], dtype=torch.int32)
+  q = rnd(b, 1, h, hd, gen=g)
+  kn = rnd(b, 1, 1, hd, gen=g)
+  vn = rnd(b, 1, 1, hd, gen=g)
+  allk = torch.cat([ck, kn], 1)
+  allv = torch.cat([cv, vn], 1)
+  mask = R.cache_mask(1, nt, window)
+  lg = torch.einsum("btnh,bsh->bnts", q, allk[:, :, 0]) * hd ** -0.5
+  lg = torch.where(mask[:, None], lg, R.MIN_LOGIT).float()
+  want = torch.einsum("bnts,bsh->btnh", torch.softmax(lg, -1).to(BF), allv[:, :, 0])
+  ckd, cvd, ntd = ck.view(b, window, hd).to(dev), cv.view(b, window, hd).to(dev), nt.to(dev)
+  got = ops.ops.local_attention_decode_(q.to(dev).view(b, h * hd), kn.to(dev).view(b, hd),
+                                        vn.to(dev).view(b, hd), ckd, cvd, ntd, h)
+  assert_close_bf16(got.view(b, 1, h, hd), want, rtol=3e-2, atol=3e-2,
+                    what=f"decode attention b={b} ctx={ctx}")
+  assert rel_l2(got.view(b, 1, h, hd), want) < 1e-2
+  ckr, cvr = ck.view(b, window, hd).clone(), cv.view(b, window, hd).clone()
+  for i in range(b):
+    ckr[i, int(nt[i]) % window] = kn[i, 0, 0]
+    cvr[i, int(nt[i]) % window] = vn[i, 0, 0]
+  assert torch.equal(ckd.cpu(), ckr) and torch.equal(cvd.cpu(), cvr)
+  assert torch.equal(ntd.cpu(), nt + 1)
+  # replays are bit-identical (fixed combine order)
+  again = ops.ops.local_attention_decode_(
+      q.to(dev).view(b, h * hd), kn.to(dev).view(b, hd), vn.to(dev).view(b, hd),
+      ck.view(b, window, hd).to(dev), cv.view(b, window, hd).to(dev), nt.to(dev), h)
+  assert torch.equal(again.cpu(), got.cpu())
+
+
 def test_kv_cache_fill_and_decode(dev):
   g = torch.Generator().manual_seed(10)
   b, h, hd, window = 3, 4, 256, 64

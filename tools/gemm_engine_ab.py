@@ -1,5 +1,6 @@
 """A/B of the prefill GEMM engines (cadence_gemm_set_engine: 0 = 8-wave
-gemm_big_kernel, 1 = 4-wave gemm_w4_kernel) on the bench shapes: outputs
+gemm_big_kernel only, 1 = the shipped plan with the 4-wave gemm_w4_kernel for
+long K) on the bench shapes: outputs
 compared bitwise, device time per launch from hipGraph replays, rounds
 interleaved in one process (uniform [-1, 1) operands).
 usage: python tools/gemm_engine_ab.py [rounds]"""
@@ -73,10 +74,10 @@ def main():
       for eng in (0, 1):
         lib.cadence_gemm_set_engine(eng)
         times.setdefault((name, eng), []).append(timeit(run))
-  lib.cadence_gemm_set_engine(0)
+  lib.cadence_gemm_set_engine(1)
   for name, flops, run, grab in cases:
     t0, t1 = (sorted(times[(name, e)])[len(times[(name, e)]) // 2] for e in (0, 1))
-    print(f"{name:34s} 8-wave {t0:8.1f} us {flops / t0 / 1e6:7.1f} TF/s | 4-wave "
+    print(f"{name:34s} 8-wave {t0:8.1f} us {flops / t0 / 1e6:7.1f} TF/s | plan   "
           f"{t1:8.1f} us {flops / t1 / 1e6:7.1f} TF/s  ({t0 / t1:.3f}x)", flush=True)
 
 
