@@ -87,6 +87,8 @@ def parse():
   ap.add_argument("--no-kernel-timing", action="store_true")
   ap.add_argument("--text-only", action="store_true", default=None,
                   help="C2-style text-only run (no vision tower)")
+  ap.add_argument("--gemm-engine", type=int, default=None,
+                  help="lab A/B: prefill GEMM engine plan (cadence_gemm_set_engine)")
   args = ap.parse_args()
   for k, v in CONFIGS[args.config].items():
     if getattr(args, k) is None:
@@ -328,6 +330,9 @@ def main():
     print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
   dev = torch.device("cuda", local)
   torch.cuda.set_device(dev)
+  if args.gemm_engine is not None:
+    from cadence import _lib
+    _lib.load().cadence_gemm_set_engine(args.gemm_engine)
   cfg, vis, model = build_model(dev, args.image_size, args.text_only)
   n_vis = 0 if vis is None else vis.n_visual_tokens
   strong = bool(args.global_batch)
@@ -438,7 +443,8 @@ def main():
     # dominant kernel: the single-stream GEMM key with the most time in the
     # step (ViT-tower launches share the GPU between two streams: their keys
     # carry a " [vit, 2 streams]" suffix and are reported, not ranked)
-    gemm_keys = [k for k in ksum if k.startswith("gemm_big_kernel") and "[" not in k]
+    gemm_keys = [k for k in ksum if k.startswith(("gemm_big_kernel", "gemm_w4_kernel"))
+                 and "[" not in k]
     dom = max(gemm_keys, key=lambda k: ksum[k]["total_ms"]) if gemm_keys else None
     # the prefill scan: the sequential kernel (B * E / 2 lanes fill the chip)
     # or the T-chunked one (small batches)
@@ -503,8 +509,8 @@ def main():
         "roofline_image_preprocess": img_iso,
         "roofline_by_kernel": {k: roofline_entry(ksum, k, "mfma", args.config)
                                for k in sorted(ksum)
-                               if k.startswith(("gemm_big", "vit_attn", "flash_attn",
-                                                "griffin_attn"))},
+                               if k.startswith(("gemm_big", "gemm_w4", "vit_attn",
+                                                "flash_attn", "griffin_attn"))},
         # a seeded 1/sample of the launches is event-timed (TIMER.sample)
         "kernels": {k: {"launches_timed": v["launches"],
                         "avg_us": round(v["avg_ms"] * 1e3, 2),

@@ -33,6 +33,7 @@ _SIGS: dict[str, list] = {
     "cadence_gemm_tile_rows": [I64, I64, I64, I64],
     "cadence_gemm_big_splits": [I64, I64, I64, I64],
     "cadence_gemm_set_engine": [I32],
+    "cadence_gemm_engine": [I64, I64, I64, I64],
     "cadence_gemm_linear": [P, I64, P, I64, P, P, I64, P, I64, I64, I64, I64,
                             I32, I64, I64, I64, P, I64, P],
     "cadence_gemm_gated_gelu": [P, I64, P, I64, P, P, P, I64, I64, I64, I64, P,

@@ -23,6 +23,7 @@ import torch
 from torch import nn
 
 from . import common, layers, modules, ops
+from .tracing import trace
 from .layers import _flat
 from .vision import MLPProjector, VisionEncoder
 
@@ -109,8 +110,10 @@ class Griffin(nn.Module):
                       device=dev)
       feats = torch.empty(b * n_vis, self.vision_config.feature_width,
                           dtype=torch.bfloat16, device=dev)
-      self.vis_encoder.features_into(self._pixels(images, img_path, b), feats)
-      self.projector.project_into(feats, x, row_map=(n_vis, length, 0))
+      with trace("vision_encoder"):
+        self.vis_encoder.features_into(self._pixels(images, img_path, b), feats)
+      with trace("projector"):
+        self.projector.project_into(feats, x, row_map=(n_vis, length, 0))
       self.embedder.encode_into(tokens, x, row_map=(t, length, n_vis))
       pos = ops.ops.splice_positions(pos, n_vis)
       return x, pos, length
@@ -131,9 +134,10 @@ class Griffin(nn.Module):
       name = f"blocks.{i}"
       nxt = (self.blocks[i + 1].temporal_pre_norm if i + 1 < n else
              (self.final_norm if final_norm else None))
-      x, xn, new_cache[name] = block.fused(
-          x, pos, b, length, None if cache is None else cache[name],
-          return_cache, inplace_state, xn, nxt, next_lazy=i + 1 < n)
+      with trace(f"{name}:{block.temporal_block_type.name.lower()}"):
+        x, xn, new_cache[name] = block.fused(
+            x, pos, b, length, None if cache is None else cache[name],
+            return_cache, inplace_state, xn, nxt, next_lazy=i + 1 < n)
     if final_norm and xn is None:
       xn = ops.rmsnorm(x, self.final_norm.scale, self.final_norm.eps,
                        packed=True)

@@ -27,6 +27,7 @@ from torch import nn
 
 from . import common, layers, ops
 from .layers import PackCache, _flat, positions_2d
+from .tracing import trace
 
 
 class RecurrentBlockCache(NamedTuple):
@@ -259,7 +260,8 @@ class RecurrentBlock(nn.Module):
         x_br, pos, None if cache is None else cache.conv1d_state, b, t)
     a, nx = self.rg_lru.gates(conv_out, pos.view(-1))
     h0 = None if cache is None else cache.rg_lru_state
-    gated, h_last = ops.ops.rnn_scan(nx, a, None, h0, y_br, b, t)
+    with trace("rnn_scan"):
+      gated, h_last = ops.ops.rnn_scan(nx, a, None, h0, y_br, b, t)
     out, hn = _out_proj(gated, self.linear_out, resid2d, norm)
     if not return_cache:
       return out, hn, None

@@ -152,13 +152,16 @@ def _tile(M: int) -> bool:
 
 def _big_key(epi: str, M: int, N: int, K: int, groups: int = 1) -> str:
   """The rocprof name of the prefill GEMM kernel a launch runs:
-  gemm_big_kernel<Epi, P8, MR> (tile height 32 MR, cadence_gemm_tile_rows)."""
+  gemm_w4_kernel<Epi, MR> or gemm_big_kernel<Epi, P8, MR> (tile height
+  32 MR, cadence_gemm_tile_rows; engine from cadence_gemm_engine)."""
   lib = _lib.load()
   rows = lib.cadence_gemm_tile_rows(M, N, K, groups)
   p8 = 1 if K % 128 == 0 else 0
   sk = lib.cadence_gemm_big_splits(M, N, K, groups)
   if sk > 1:   # split-K launch pair: partial GEMM + the epilogue's reduce
     return f"gemm_big_kernel<EpiPartial, {p8}, {rows // 32}> + splitk_reduce<{epi}> (split {sk})"
+  if lib.cadence_gemm_engine(M, N, K, groups):
+    return f"gemm_w4_kernel<{epi}, {rows // 32}>"
   return f"gemm_big_kernel<{epi}, {p8}, {rows // 32}>"
 
 
@@ -1004,6 +1007,8 @@ def _vit_prefix(tokens, resid, B, ntok, prefix):
 @_reg("vit_attention(Tensor qkv, int B, int N, int H, int hd) -> Tensor")
 def _vit_attention(qkv, B, N, H, hd):
   _need(qkv.is_contiguous() and qkv.dtype == _BF16, "qkv contiguous bf16")
+  if qkv.data_ptr() % 16:      # the kernels load 16-B rows (C-ABI contract)
+    qkv = qkv.clone()
   out = torch.empty(B * N, H * hd, dtype=_BF16, device=qkv.device)
   ev = TIMER.start(qkv)
   _lib.check(_lib.load().cadence_vit_attention(

@@ -35,6 +35,7 @@ from typing import Generic, NamedTuple, Sequence, TypeVar
 import torch
 
 from . import common, ops
+from .tracing import trace
 from .modules import AttentionBlockCache
 
 Cache = TypeVar("Cache")
@@ -169,9 +170,10 @@ class Sampler:
     graph_first = (t > 1 and self.use_graph and self.greedy_sampling and
                    not return_logits and steps > 2)
     if t > 1:
-      prev_logits, cache = self.apply_model(tokens[:, :-1], positions[:, :-1],
-                                            None, return_logits and echo, True,
-                                            img_path, images, splice)
+      with trace("sampler:prefill"):
+        prev_logits, cache = self.apply_model(tokens[:, :-1], positions[:, :-1],
+                                              None, return_logits and echo, True,
+                                              img_path, images, splice)
       if events is not None:
         events["prefill_end"].record()
       if graph_first:
@@ -436,11 +438,12 @@ class _DecodeGraph:
         events["decode_steps"] = n_more
         events["decode_start"].record()
       done = 0
-      for i in range(n_more):
-        if watch.finished(i):
-          break
-        self.graph.replay()
-        done += 1
+      with trace("sampler:decode"):
+        for i in range(n_more):
+          if watch.finished(i):
+            break
+          self.graph.replay()
+          done += 1
       if events is not None:
         events["decode_end"].record()
     dev_stream.wait_stream(self.stream)

@@ -10,7 +10,9 @@
 //     to bf16 then * hd^-0.5, mask = same segment & causal & window; key
 //     tiles outside [max(seg_start, q0 - W), q_last] are skipped.  MQA: every
 //     head reads the single K/V head.
-//   MODE_VIT: timm bidirectional SDPA (fp32 logits, no mask but the tail).
+//   MODE_VIT: timm bidirectional SDPA (fp32 logits, no mask but the tail);
+//     not instantiated: cadence_vit_attention runs vit_attention.hip /
+//     vit_stream_attn_kernel for every shape it accepts.
 // decode_attn_kernel: one wave per sequence, 16 rows = the query heads,
 // keys = ring-buffer slots (positions of _compute_cache_mask) + the new key,
 // then the in-place slot update of _update_attention_cache.
@@ -807,24 +809,11 @@ int cadence_vit_attention(const void* qkv, void* out, int64_t B, int64_t N,
     const int rc = vit_attention_lds_launch(qkv, out, B, N, H, hd, stream);
     if (rc >= 0) return rc;
   }
-  // longer sequences (336 / 384 px towers): K/V tiles streamed by LDS-DMA
-  {
-    const int rc = vit_stream_attention_launch(qkv, out, B, N, H, hd, stream);
-    if (rc >= 0) return rc;
-  }
-  const int64_t D = H * hd;
-  AttnArgs a{};
-  const u16* base = static_cast<const u16*>(qkv);
-  a.q = base; a.q_bs = N * 3 * D; a.q_rs = 3 * D; a.q_hs = hd;
-  a.k = base + D; a.k_bs = N * 3 * D; a.k_rs = 3 * D; a.k_hs = hd;
-  a.v = base + 2 * D; a.v_bs = N * 3 * D; a.v_rs = 3 * D; a.v_hs = hd;
-  a.o = static_cast<u16*>(out); a.o_bs = N * D; a.o_rs = D; a.o_hs = hd;
-  a.L = (int)N; a.H = (int)H; a.hd = (int)hd; a.window = 0;
-  a.scale = 1.0f / sqrtf((float)hd);
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  if (hd == 64) launch_flash<64, MODE_VIT>(a, (int)B, st);
-  else launch_flash<96, MODE_VIT>(a, (int)B, st);
-  return (int)hipGetLastError();
+  // longer sequences (336 / 384 px towers): K/V tiles streamed by LDS-DMA;
+  // it takes every shape but a qkv / out pointer that is not 16-B aligned,
+  // which the contract excludes (cadence_kernels.h)
+  const int rc = vit_stream_attention_launch(qkv, out, B, N, H, hd, stream);
+  return rc >= 0 ? rc : (int)hipErrorInvalidValue;
 }
 
 int cadence_kv_cache_fill(const void* k, const void* v,

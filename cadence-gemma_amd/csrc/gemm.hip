@@ -1971,6 +1971,21 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
 
 int g_engine = 1;   // lab A/B switch of the prefill engine (0 = 8-wave only)
 
+// The 4-wave engine runs the wide long-K GEMMs (the gated MLP up-projection,
+// N = 2F = 15360, K = 2560) on 224 / 256-row tile plans.  Measured A/B in
+// the bench pipeline (tools/bench_engine_ab.sh, profiles/r03f_*): gated
+// 717 vs 734 us; the N = 2560..5120 projections ran 10 % SLOWER on it there
+// (288 vs 263 us) although 4 % faster in isolation with warm operands: one
+// wave per SIMD and one K-tile of DMA lookahead expose the cold weight
+// panels' HBM latency that the 8-wave engine's two waves per SIMD and 1.5
+// K-tiles in flight hide.  A 5-slot 32-deep ring with 1.5 K-tiles of
+// lookahead was slower still (barrier per 32-deep step; profiles/r03g_*).
+// Short K keeps the 8-wave engine, whose 8 waves also finish element-wise
+// epilogues twice as fast (fc1's erf-GELU at K = 1024: 0.87x on 4 waves).
+bool use_w4(int64_t N, int64_t K, int rows) {
+  return g_engine != 0 && K >= 2048 && N >= 8192 && (rows == 224 || rows == 256);
+}
+
 // Prefill engine plan for M > kSkinnyMaxM: 0 = 2-buffer 256-row kernel,
 // 160 / 192 / 224 / 256 = 8-phase kernel with that tile height.
 //  * 8-phase when K splits into pairs of 64-deep tiles (an A/B of the
@@ -2080,10 +2095,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                          parts, sk, 1, (int)M, (int)N, epi);
       return (int)hipGetLastError();
     }
-    // long-K GEMMs whose tile plan is 224 or 256 rows run on the 4-wave
-    // engine (its MFMA loop is 6-9 % faster there); short K keeps the 8-wave
-    // engine, whose 8 waves finish the element-wise epilogues twice as fast
-    if (g_engine != 0 && K >= 2048 && (rows == 224 || rows == 256)) {
+    if (use_w4(N, K, rows)) {
       const dim3 wgrid((unsigned)(((M + rows - 1) / rows) * ((N + 255) / 256)),
                        (unsigned)groups);
       if constexpr (std::is_same_v<Epi, EpiLinear>) {
@@ -2220,6 +2232,14 @@ int cadence_gemm_big_splits(int64_t M, int64_t N, int64_t K, int64_t groups) {
   if (M <= kSkinnyMaxM || M <= 0) return 1;
   const int64_t g = groups > 0 ? groups : 1;
   return big_splits(M, N, K, g, big_tile_rows(M, N, K, g));
+}
+
+int cadence_gemm_engine(int64_t M, int64_t N, int64_t K, int64_t groups) {
+  if (M <= kSkinnyMaxM || M <= 0) return 0;
+  const int64_t g = groups > 0 ? groups : 1;
+  const int rows = big_tile_rows(M, N, K, g);
+  if (big_splits(M, N, K, g, rows) > 1) return 0;
+  return use_w4(N, K, rows) ? 1 : 0;
 }
 
 int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {

@@ -65,11 +65,19 @@ __global__ __launch_bounds__(256) void conv1d_prefill_kernel(
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = badd(acc[i], bv[i]);
     st16(out + ((int64_t)b * L + t) * ldo + e0, pack8(acc));
-    // new state = last TW-1 inputs, left-padded with zeros when L < TW-1
+    // new state = last TW-1 inputs, left-padded with zeros when L < TW-1.
+    // compat (Q4): the reference zeroes masked rows of x in place before
+    // caching x[:, 1-TW:] (layers.py:506,524,542); cache row t = L - m was
+    // zeroed by shift m - 1 iff pos[t + k] == 0 for some k in 1..m-3 (only
+    // reachable for TW > 4)
     if (cache_out && t >= L - (TW - 1)) {
       const int slot = t - (L - (TW - 1));
+      bool keep = true;
+      if (compat)
+        for (int k = 1; k <= L - t - 3; ++k)
+          keep = keep && (pos[(int64_t)b * L + t + k] != 0);
       st16(cache_out + ((int64_t)b * (TW - 1) + slot) * E + e0,
-           ld16(x + ((int64_t)b * L + t) * ldx + e0));
+           keep ? ld16(x + ((int64_t)b * L + t) * ldx + e0) : make_uint4(0, 0, 0, 0));
     }
     if (cache_out && t == 0 && L < TW - 1) {
       for (int slot = 0; slot < TW - 1 - L; ++slot)

@@ -87,6 +87,11 @@ int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups);
  * the epilogue to the split-order sums.  Host-only arithmetic. */
 int cadence_gemm_big_splits(int64_t M, int64_t N, int64_t K, int64_t groups);
 
+/* The prefill engine a launch of this shape takes: 1 = the 4-wave
+ * gemm_w4_kernel<Epi, rows / 32>, 0 = gemm_big_kernel (or, M <= 64, the
+ * decode engines).  Host-side plan query. */
+int cadence_gemm_engine(int64_t M, int64_t N, int64_t K, int64_t groups);
+
 /* Lab A/B switch of the prefill engine: 1 (default) = the shipped plan (the
  * 4-wave gemm_w4_kernel for K >= 2048 on 224 / 256-row tile plans, else the
  * 8-wave gemm_big_kernel), 0 = 8-wave only; returns the previous value.
@@ -389,7 +394,8 @@ int cadence_vit_prefix(const void* tokens, float* resid, int64_t B,
                        int64_t ntok, int64_t prefix, int64_t D, void* stream);
 
 /* Bidirectional multi-head attention (timm Attention, fused SDPA):
- * qkv [B*N, 3*H*hd] bf16 -> out [B*N, H*hd] bf16; hd in {64, 72}. */
+ * qkv [B*N, 3*H*hd] bf16 -> out [B*N, H*hd] bf16; hd in {64, 72}; qkv and
+ * out 16-B aligned (returns hipErrorInvalidValue otherwise). */
 int cadence_vit_attention(const void* qkv, void* out, int64_t B, int64_t N,
                           int64_t H, int64_t hd, void* stream);
 

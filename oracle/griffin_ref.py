@@ -99,7 +99,7 @@ def conv1d(x, segment_pos, w, b, cache=None, compat: bool = True):
     prompt = width - 1
     cache_dtype = cache.dtype
   else:
-    full = x.clone()           # the reference masks a view of x in place (Q4)
+    full = x.clone()           # the reference masks views of x in place (Q4)
     prompt = 0
     cache_dtype = x.dtype
   notb = (segment_pos != 0)
@@ -115,7 +115,15 @@ def conv1d(x, segment_pos, w, b, cache=None, compat: bool = True):
       m = torch.ones(win.shape[:2], dtype=torch.bool)
       for k in looks:
         m = m & notb[:, lo + k: hi + k]
-      win = win * m[..., None].to(x.dtype)
+      if compat:
+        # layers.py:506,524: `x_window *= mask` on a view of x, so the
+        # zeroed rows stay zero for the later shifts (no effect there: their
+        # masks are supersets) and in the cache x[:, 1-width:] (:542) -- rows
+        # L-7..L-4 of a width-8 cache when a document starts near the end
+        full[:, lo:hi] *= m[..., None].to(x.dtype)
+        win = full[:, lo:hi]
+      else:
+        win = win * m[..., None].to(x.dtype)
     if win.shape[1] < out_len:
       pad = torch.zeros(win.shape[0], out_len - win.shape[1], win.shape[2],
                         dtype=win.dtype)

@@ -175,3 +175,18 @@ def test_prefill_gemm_plan_host_arithmetic():
   assert splits(319, 2560, 2560, 8) == 1               # grouped launches never split
   s = splits(319, 2560, 7680, 1)
   assert lib.cadence_gemm_workspace_bytes(319, 2560, 7680, 1) == s * 319 * 2560 * 4
+
+
+def test_roctx_ranges_nest():
+  """SURVEY §5 tracing: the roctx ranges are opt-in and nest (push / pop)."""
+  from cadence import tracing
+  prev = tracing.enabled()
+  tracing.enable(True)
+  try:
+    with tracing.trace("outer"):
+      with tracing.trace("inner"):
+        pass
+  finally:
+    tracing.enable(prev)
+  assert tracing.enabled() == prev
+

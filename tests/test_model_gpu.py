@@ -169,19 +169,23 @@ def test_forward_equivalence(dev):
                              rtol=1e-4, atol=1e-2)
 
 
-def tiny_vision(image_size=56):
+def tiny_vision(image_size=56, gelu_tanh=False):
   dino = common.ViTConfig(name="dino", width=1024, depth=2, num_heads=16,
                           mlp_width=4096, class_token=True, reg_tokens=4,
                           layer_scale=True)
   sig = common.ViTConfig(name="siglip", width=1152, depth=2, num_heads=16,
-                         mlp_width=4304, mean=common.SIGLIP_MEAN,
-                         std=common.SIGLIP_STD)
+                         mlp_width=4304, gelu_tanh=gelu_tanh,
+                         mean=common.SIGLIP_MEAN, std=common.SIGLIP_STD)
   return common.VisionConfig(image_size=image_size, dino=dino, siglip=sig,
                              feature_block=1)
 
 
-def test_vision_and_projector_vs_oracle(dev):
-  vis = tiny_vision()
+@pytest.mark.parametrize("gelu_tanh", [False, True])
+def test_vision_and_projector_vs_oracle(dev, gelu_tanh):
+  """Both towers + projector; gelu_tanh=True is the SigLIP MLP of the
+  original big_vision model (SURVEY §8c flag; timm's default is erf):
+  the fc1 epilogue's act 3."""
+  vis = tiny_vision(gelu_tanh=gelu_tanh)
   cfg = small_config()
   m, p = make_model(dev, cfg, seed=9, vision=vis)
   with torch.no_grad():   # make LayerScale matter

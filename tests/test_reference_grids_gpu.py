@@ -159,3 +159,25 @@ def test_conv1d_grid(dev, width, temporal_width):
     want, c_ref = R.conv1d(y[:, i:i + 1], sp, p["w"], p["b"], c_ref)
     got, c = conv(y[:, i:i + 1].to(dev), sp.to(dev), c)
     assert torch.equal(got.cpu(), want) and torch.equal(c.cpu(), c_ref)
+
+
+@pytest.mark.parametrize("temporal_width", [4, 8])
+@pytest.mark.parametrize("start", [3, 5, 6, 7])
+def test_conv1d_cache_late_document(dev, temporal_width, start):
+  """Appendix A Q4: a document starting `start` tokens before the end.  The
+  reference zeroes masked rows of x in place (layers.py:506,524) before it
+  caches x[:, 1-width:] (:542), so a width-8 cache loses rows L-7..L-4 ahead
+  of the new document; width 4 never does.  Bit-exact with the oracle."""
+  g = torch.Generator().manual_seed(55 + temporal_width + start)
+  width, L = 128, 32
+  conv = cadence.Conv1D(width, temporal_width, device=dev, dtype=BF)
+  p = _params(conv, g, scale=1.0)
+  x = torch.randn(2, L, width, generator=g).to(BF)
+  pos = torch.arange(L, dtype=torch.int32)[None].repeat(2, 1)
+  pos[0, L - start:] = torch.arange(start, dtype=torch.int32)   # new document
+  want, c_ref = R.conv1d(x, pos, p["w"], p["b"])
+  got, c = conv(x.to(dev), pos.to(dev))
+  assert torch.equal(got.cpu(), want) and torch.equal(c.cpu(), c_ref)
+  if temporal_width == 8 and start <= 5:
+    assert not torch.equal(c_ref[0], x[0, 1 - temporal_width:])   # Q4 reached
+

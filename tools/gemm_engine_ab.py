@@ -36,10 +36,38 @@ def u(*shape, dev):
   return (torch.rand(*shape, device=dev) * 2 - 1).to(BF)
 
 
+def ksweep(dev, lib):
+  """M = 10240, N = 15360, K = 512 .. 5120 on both engines: time = fixed +
+  per-K slope (the engines' per-tile fixed cost vs main-loop rate)."""
+  M, N = 10240, 15360
+  res = {}
+  for K in (512, 1024, 2048, 2560, 4096, 5120):
+    a, w = u(M, K, dev=dev), (u(N, K, dev=dev) * (1.0 / K ** 0.5)).to(BF)
+    out = torch.empty(M, N, device=dev, dtype=BF)
+    for eng in (0, 1):
+      lib.cadence_gemm_set_engine(eng)
+      t = timeit(lambda: ops.linear(a, w, out=out))
+      res[(K, eng)] = t
+      print(f"ksweep K={K:5d} engine {eng}: {t:8.1f} us  {2 * M * N * K / t / 1e6:7.1f} TF/s",
+            flush=True)
+  lib.cadence_gemm_set_engine(1)
+  for eng in (0, 1):
+    ks = sorted({k for k, e in res if e == eng})
+    xs = torch.tensor(ks, dtype=torch.float64)
+    ys = torch.tensor([res[(k, eng)] for k in ks], dtype=torch.float64)
+    slope = float(((xs - xs.mean()) * (ys - ys.mean())).sum() / ((xs - xs.mean()) ** 2).sum())
+    icpt = float(ys.mean() - slope * xs.mean())
+    print(f"ksweep engine {eng}: fixed {icpt:.1f} us + {slope:.4f} us per unit K "
+          f"({2 * M * N / slope / 1e6:.0f} TF/s marginal)", flush=True)
+
+
 def main():
   rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
   dev = torch.device("cuda")
   lib = _lib.load()
+  if len(sys.argv) > 2 and sys.argv[2] == "ksweep":
+    ksweep(dev, lib)
+    return
   cases = []
   for M, N, K, act in ((10208, 5120, 2560, 0), (10208, 2560, 7680, 0),
                        (8352, 3072, 1024, 0), (8352, 4096, 1024, 1),
