@@ -119,13 +119,15 @@ class Sampler:
                total_generation_steps: int, images=None, img_path=None,
                return_logits: bool = False, echo: bool = False,
                end_sampling_at_eos_token: bool = False,
-               events: dict | None = None) -> SamplingState:
+               events: dict | None = None, slot: int = 0) -> SamplingState:
     """Prefill + decode for a left-padded [B, T] prompt batch (on device).
 
     `events`, if given, receives HIP events bracketing the prefill
     ("prefill_start"/"prefill_end") and the graph-replayed decode steps
-    ("decode_start"/"decode_end", with "decode_steps") on the decode
-    graph's stream.
+    ("decode_start"/"decode_end", with "decode_steps").  Everything runs
+    on the caller's current stream (the decode graph is replayed there);
+    `slot` picks the decode graph (static buffers) -- calls that may overlap
+    on different streams must use different slots (`generate_many`).
     """
     dev = self.device
     b, t = tokens.shape
@@ -184,7 +186,7 @@ class Sampler:
         cur = tokens[:, -1].to(torch.int32).contiguous()
         done = self._decode_graph(cur, pos, cache, buf, step, steps,
                                   eos_stop, events, start=0,
-                                  cache_len=n_img + t - 1)
+                                  cache_len=n_img + t - 1, slot=slot)
         if echo:
           buf = torch.cat([tokens, buf], dim=1)
         return SamplingState(buf, step, torch.tensor(steps), pos[:, None], cache,
@@ -220,7 +222,7 @@ class Sampler:
     if graphable:
       done = self._decode_graph(cur, pos, cache, buf, step, n_more,
                                 eos_stop, events,
-                                cache_len=n_img + t, done_in=dflags)
+                                cache_len=n_img + t, done_in=dflags, slot=slot)
     else:
       watch = _DoneWatch(dflags)
       for i in range(n_more):
@@ -246,6 +248,45 @@ class Sampler:
     return SamplingState(buf, step, torch.tensor(steps), pos[:, None], cache,
                          done, lbuf)
 
+  @torch.no_grad()
+  def generate_many(self, batches: Sequence[tuple], total_generation_steps: int,
+                    lanes: int = 2, events: dict | None = None
+                    ) -> list[SamplingState]:
+    """Generation for a sequence of micro-batches, pipelined over `lanes`
+    streams: micro-batch j runs whole (prefill, then its decode graph
+    replays) on lane j % lanes, so one lane's prefill (MFMA-bound GEMMs, plus
+    the vision tower's side stream) overlaps another lane's decode steps (a
+    latency-bound GEMV chain) on the GPU.  Each lane has its own decode graph
+    (static buffers, arrival counters).  `batches`: (tokens [B, T],
+    input_lengths [B], images or None) per micro-batch; the outputs equal
+    `generate` on each in turn.  `events` applies to the last micro-batch.
+    Returns the states, ready on the caller's stream."""
+    dev = self.device
+    cur = torch.cuda.current_stream(dev)
+    ls = self.__dict__.setdefault("_lanes", {})
+    streams = ls.setdefault(dev, [])
+    while len(streams) < lanes:
+      streams.append(torch.cuda.Stream(device=dev))
+    streams = streams[:lanes]
+    for s in streams:
+      s.wait_stream(cur)
+    states = []
+    for j, (tokens, lengths, images) in enumerate(batches):
+      ev = events if j == len(batches) - 1 else None
+      with torch.cuda.stream(streams[j % lanes]):
+        states.append(self.generate(tokens, lengths, total_generation_steps,
+                                    images=images, events=ev, slot=j % lanes))
+    for s in streams:
+      cur.wait_stream(s)
+    for st in states:   # allocated on a lane stream, handed to the caller's
+      for t in (st.tokens_buffer, st.step, st.positions, st.done):
+        if t.is_cuda:
+          t.record_stream(cur)
+      for v in (st.cache or {}).values():
+        for t in v:
+          t.record_stream(cur)
+    return states
+
   def _sample(self, logits: torch.Tensor) -> torch.Tensor:
     if self.greedy_sampling:
       return torch.argmax(logits, dim=-1).to(torch.int32)
@@ -269,15 +310,16 @@ class Sampler:
     ops.ops.decode_advance_(nxt, buf, step, pos, cur, dflags, *self._eos_args())
 
   def _decode_graph(self, cur, pos, cache, buf, step, n_more, eos_stop,
-                    events=None, start=1, cache_len=None, done_in=None):
+                    events=None, start=1, cache_len=None, done_in=None, slot=0):
     """Replays a captured single-token decode step `n_more` times.
 
     The graph holds raw pointers to the model's (packed) weights, so it is
     keyed on the parameters' storage and version counters: a weight reload
-    or in-place update recaptures it."""
+    or in-place update recaptures it.  One graph per `slot` (its own static
+    buffers and capture stream, hence its own arrival counters)."""
     if not hasattr(self, "_graphs"):
       self._graphs = {}
-    key = (cur.shape[0], cur.device, bool(eos_stop))
+    key = (cur.shape[0], cur.device, bool(eos_stop), slot)
     version = tuple((p.data_ptr(), p._version) for p in self.model.parameters())
     eng = self._graphs.get(key)
     if eng is None or eng.max_steps < buf.shape[1] or eng.version != version:
@@ -366,7 +408,9 @@ class _DecodeGraph:
   EOS flags and a private copy of every block cache (recurrent states and
   attention ring buffers are updated in place by the kernels).  `run`
   copies the prefill state in, replays the graph, and copies the generated
-  tokens out.
+  tokens out, all on the caller's current stream.  Capture happens on a
+  private stream (hipGraph capture cannot use the null stream), which also
+  keys the graph's own arrival counters.
   """
 
   def __init__(self, model, cache_like, batch, max_steps, device, eos_stop,
@@ -417,7 +461,6 @@ class _DecodeGraph:
     tokens before it are already in `buf`, the rest of `buf` is pad).
     `cache_len`: tokens already in the attention caches (host-known), so
     only written ring slots move.  Returns the per-row done flags."""
-    dev_stream = torch.cuda.current_stream(cur.device)
     steps = buf.shape[1]
     self._copy_cache(self.cache, cache, cache_len)
     self.cur.copy_(cur)
@@ -430,23 +473,20 @@ class _DecodeGraph:
       else:
         self.done.zero_()
     watch = _DoneWatch(self.done)
-    self.stream.wait_stream(dev_stream)
-    with torch.cuda.stream(self.stream):
-      if events is not None:   # the replays alone (cache copies excluded)
-        events["decode_start"] = torch.cuda.Event(enable_timing=True)
-        events["decode_end"] = torch.cuda.Event(enable_timing=True)
-        events["decode_steps"] = n_more
-        events["decode_start"].record()
-      done = 0
-      with trace("sampler:decode"):
-        for i in range(n_more):
-          if watch.finished(i):
-            break
-          self.graph.replay()
-          done += 1
-      if events is not None:
-        events["decode_end"].record()
-    dev_stream.wait_stream(self.stream)
+    if events is not None:   # the replays alone (cache copies excluded)
+      events["decode_start"] = torch.cuda.Event(enable_timing=True)
+      events["decode_end"] = torch.cuda.Event(enable_timing=True)
+      events["decode_steps"] = n_more
+      events["decode_start"].record()
+    done = 0
+    with trace("sampler:decode"):
+      for i in range(n_more):
+        if watch.finished(i):
+          break
+        self.graph.replay()
+        done += 1
+    if events is not None:
+      events["decode_end"].record()
     buf[:, start:].copy_(self.buf[:, start:steps])
     step.copy_(self.step)
     pos.copy_(self.pos)

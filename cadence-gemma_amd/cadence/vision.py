@@ -244,9 +244,11 @@ class VisionEncoder(nn.Module):
     `out2d`, so SigLIP runs on a side stream beside DINO: the two towers'
     GEMMs (132-160 output tiles each at bs=32, 224 px) fill the 256 CUs
     together where either alone leaves ~40 % of them idle.  Not while a
-    graph is being captured (one stream there)."""
+    graph is being captured (one stream there), nor with `two_streams` set
+    False on the encoder."""
     n = self.config.blocks_run
-    if torch.cuda.is_current_stream_capturing() or not pixels.is_cuda:
+    if (torch.cuda.is_current_stream_capturing() or not pixels.is_cuda or
+        not self.__dict__.get("two_streams", True)):
       self.dino.features_into(pixels, out2d, 0, n)
       self.siglip.features_into(pixels, out2d, self.config.dino.width, n)
       return

@@ -271,3 +271,40 @@ def test_decode_graph_reuse_partial_cache_copies(dev):
       else:
         for a, b in zip(ce, cg):
           assert torch.equal(a, b), name
+
+
+def test_generate_many_pipeline_matches_sequential(dev):
+  """Sampler.generate_many (micro-batch j + 1's prefill issued while j
+  decodes, two decode-graph slots on the decode stream) gives exactly the
+  tokens, positions and caches of one generate per micro-batch, with images
+  (the vision side stream) and ragged prompts; the sampler is reused so both
+  slots are overwritten by later micro-batches."""
+  vis = tiny_vision()
+  cfg = small_config(window=64)
+  m, _ = make_model(dev, cfg, seed=31, vision=vis)
+  vocab = MockVocab()
+  g = torch.Generator().manual_seed(32)
+  b, t, steps = 4, 12, 9
+  batches = []
+  for j in range(5):
+    tok = torch.randint(3, cfg.vocab_size, (b, t), generator=g, dtype=torch.int32)
+    lens = torch.tensor([t, t - 1 - j % 3, t, 5], dtype=torch.int32)
+    for i, n in enumerate(lens.tolist()):
+      tok[i, :t - n] = 0
+    px = torch.rand(b, 3, 56, 56, generator=g)
+    batches.append((tok.to(dev), lens, px.to(dev)))
+  seq = cadence.Sampler(m, vocab, use_graph=True)
+  want = [seq.generate(tk, ln, steps, images=px) for tk, ln, px in batches]
+  pipe = cadence.Sampler(m, vocab, use_graph=True)
+  for _ in range(2):
+    got = pipe.generate_many(batches, steps)
+    for w, gt in zip(want, got):
+      assert torch.equal(w.tokens_buffer.cpu(), gt.tokens_buffer.cpu())
+      assert torch.equal(w.positions.cpu(), gt.positions.cpu())
+      assert int(w.step) == int(gt.step)
+      for name, cw in w.cache.items():
+        for a, c in zip(cw, gt.cache[name]):
+          if a.dim() == 4:   # ring buffers: the written slots
+            n = int(cw.num_tokens.max())
+            a, c = a[:, :n], c[:, :n]
+          assert torch.equal(a, c), name
