@@ -352,8 +352,8 @@ def main():
   positions = torch.arange(args.prompt, dtype=torch.int32, device=dev)[None].repeat(
       args.batch, 1)
 
-  def step(events=None):
-    if args.decode and not args.no_pipeline:
+  def step(events=None, pipeline=True):
+    if args.decode and pipeline and not args.no_pipeline:
       # micro-batch j + 1's prefill overlaps micro-batch j's decode
       # (Sampler.generate_many); `events` time the last micro-batch
       sts = sampler.generate_many(
@@ -405,7 +405,10 @@ def main():
     o = None
     for i in range(args.steps):
       ev = {}
-      o = step(ev)
+      # the kernel-timing pass runs the micro-batches one after another: with
+      # two lanes in flight an event pair would also time the queueing behind
+      # the other lane's kernels, not the launch itself
+      o = step(ev, pipeline=not kernel_timing)
       sev[i + 1].record()
       evs.append(ev)
     torch.cuda.synchronize()
@@ -423,7 +426,8 @@ def main():
     dt, step_ev, ev_list, out = timed_pass(False)
     ksum = {}
     if not args.no_kernel_timing:
-      timed_pass(True)
+      # prefill / decode-step events from the sequential pass as well
+      _, _, ev_list, _ = timed_pass(True)
       ksum = ops.TIMER.summary()
   elapsed = D.max_over_ranks(dt)
   per_step = sorted(step_ev[i].elapsed_time(step_ev[i + 1])
@@ -515,7 +519,10 @@ def main():
         "prefill_timing": ("last micro-batch's prefill, overlapping the previous "
                            "micro-batch's decode (Sampler.generate_many)"
                            if args.decode and not args.no_pipeline and n_micro > 1
-                           else "last micro-batch's prefill"),
+                           and args.no_kernel_timing
+                           else "last micro-batch's prefill" + (
+                               " in the kernel-timing pass (micro-batches run one "
+                               "after another)" if not args.no_kernel_timing else "")),
         "prefill_tokens_per_s": round(prefill_tps, 1),
         "roofline": roofline_entry(ksum, dom, "mfma", args.config) if dom else None,
         "roofline_scan": roofline_entry(ksum, scan_key, "hbm", args.config)
@@ -534,9 +541,12 @@ def main():
                                                  args.steps, 3)}
                     for k, v in sorted(ksum.items())},
         "kernel_timing": f"HIP events on a seeded 1/{ops.TIMER.sample} of the launches "
-                         "of a second timed pass of the same K steps (the value / "
-                         "ms_per_step pass carries no per-kernel events: they cost "
-                         "the stream ~3 % of the step)",
+                         "of a second timed pass of the same K steps, micro-batches "
+                         "run one after another (the value / ms_per_step pass "
+                         "carries no per-kernel events: they cost the stream ~3 % "
+                         "of the step; it runs two micro-batch lanes whose kernels "
+                         "share the CUs, so an event pair there would time "
+                         "queueing behind the other lane)",
         "generated_tokens_checksum": int(out.long().sum().item()),
     }
     if world == 1 and not args.no_cpu_baseline:
