@@ -528,6 +528,10 @@ def main():
         "roofline_scan": roofline_entry(ksum, scan_key, "hbm", args.config)
                          if scan_key else None,
         "roofline_decode": dec,
+        # prefill RG-LRU gates: HBM-priced (x in, a and normalised x out)
+        "roofline_rglru_gates": next((roofline_entry(ksum, k, "hbm", args.config)
+                                      for k in sorted(ksum)
+                                      if k.startswith("rglru_gates_stream_kernel")), None),
         "roofline_vit_attention": vit_iso,
         "roofline_image_preprocess": img_iso,
         "roofline_by_kernel": {k: roofline_entry(ksum, k, "mfma", args.config)

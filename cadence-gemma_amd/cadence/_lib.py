@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -43,6 +43,8 @@ _SIGS: dict[str, list] = {
     "cadence_gemm_rmsnorm_workspace_bytes": [I64, I64, I64],
     "cadence_qkv_rope_decode": [P, I64, P, I64, P, P, P, P, I64, I64, I64, I64, P,
                                 I64, I32, F32, P],
+    "cadence_qkv_rope_prefill": [P, I64, P, I64, P, P, P, P, I64, I64, I64, I64, P,
+                                 I64, P],
     "cadence_gemm_linear_conv1d": [P, I64, P, I64, P, P, I64, I64, I64, I64, I64,
                                    P, P, P, I64, I32, F32, P],
     "cadence_gemm_linear_residual_rows": [P, I64, P, I64, P, P, I64, P, I64, P,

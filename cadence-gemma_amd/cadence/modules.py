@@ -125,6 +125,12 @@ class LocalAttentionBlock(nn.Module):
       # decode: RoPE runs in the q|k|v projection's epilogue
       q, k, v = ops.qkv_rope_decode(xn2d, self.qkv_weight_rope(),
                                     pos.view(-1).to(torch.int32), h, hd)
+    elif (tuned and isinstance(xn2d, torch.Tensor) and
+          ops.qkv_rope_prefill_ok(b * t, h, hd, self.width)):
+      # prompt pass: RoPE in the q|k|v GEMM's epilogue (one launch)
+      q, k, v = ops.ops.qkv_rope_prefill(xn2d, self.qkv_weight_rope(),
+                                         pos.view(-1).to(torch.int32), h, hd,
+                                         ops.rope_table(xn2d.device, hd))
     else:
       qkv = ops.linear(xn2d, self.qkv_weight())[:, :(h + 2) * hd]
       q, k, v = ops.ops.rope_qkv(qkv, pos.view(-1), h, hd,

@@ -539,8 +539,15 @@ def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos,
       E, M, H, bw, _p(ws), nws,
       _s(x)), "rglru_gates")
   if ev is not None:
-    TIMER.stop(ev, _big_key("EpiRglruGates", M, 2 * bw, bw, H),
-               2.0 * M * 2 * bw * bw * H, x)
+    if (not decode_layout and bw in (64, 128, 256) and
+        _lib.load().cadence_gemm_set_engine(-1) != 0):
+      # the block-bound streaming kernel: priced on HBM bytes (x in, a and
+      # normalised x out, the packed weights once)
+      TIMER.stop(ev, f"rglru_gates_stream_kernel<{bw}>",
+                 3.0 * M * E * 2 + w_packed.numel() * 2, x)
+    else:
+      TIMER.stop(ev, _big_key("EpiRglruGates", M, 2 * bw, bw, H),
+                 2.0 * M * 2 * bw * bw * H, x)
   return a, nx
 
 
@@ -834,6 +841,40 @@ def _qkv_rope_decode(a, w_perm, positions, H, hd, table=None, w_packed=False,
       M, H, hd, K, _p(table), tlen, _norm_flag(norm, lda), float(norm_eps),
       _s(a)), "qkv_rope_decode")
   return q, k, v
+
+
+@_reg("qkv_rope_prefill(Tensor a, Tensor w_perm, Tensor positions, int H, int hd, "
+      "Tensor? table) -> (Tensor, Tensor, Tensor)")
+def _qkv_rope_prefill(a, w_perm, positions, H, hd, table=None):
+  """Prompt-pass q|k|v GEMM with RoPE in its epilogue (one block-engine
+  launch; qkv_rope_prefill_ok() says whether the shape's plan allows it)."""
+  lda, ldw = _mat(a, "a"), _mat(w_perm, "w_perm")
+  M, K = a.shape
+  N = w_perm.shape[0]
+  _need(N == (H + 2) * hd and w_perm.shape[1] == K, "w_perm shape")
+  _need(positions.dtype == _I32 and positions.numel() == M, "positions")
+  q = torch.empty(M, H * hd, dtype=_BF16, device=a.device)
+  k = torch.empty(M, hd, dtype=_BF16, device=a.device)
+  v = torch.empty(M, hd, dtype=_BF16, device=a.device)
+  tlen = table.shape[0] if table is not None else 0
+  ev = TIMER.start(a)
+  _lib.check(_lib.load().cadence_qkv_rope_prefill(
+      _p(a), lda, _p(w_perm), ldw, _p(positions.contiguous()), _p(q), _p(k), _p(v),
+      M, H, hd, K, _p(table), tlen, _s(a)), "qkv_rope_prefill")
+  if ev is not None:
+    TIMER.stop(ev, _big_key("EpiRopeQKVBig", M, N, K), 2.0 * M * N * K, a)
+  return q, k, v
+
+
+def qkv_rope_prefill_ok(M: int, H: int, hd: int, K: int) -> bool:
+  """The fused prefill q|k|v + RoPE launch covers this shape: block engine,
+  one K split, not the 4-wave engine (host-side plan queries)."""
+  N = (H + 2) * hd
+  if M <= 64 or hd % 64 or N % 64 or K % 64:
+    return False
+  lib = _lib.load()
+  return (lib.cadence_gemm_big_splits(M, N, K, 1) == 1 and
+          lib.cadence_gemm_engine(M, N, K, 1) == 0)
 
 
 def qkv_rope_permutation(H: int, hd: int, device=None) -> torch.Tensor:

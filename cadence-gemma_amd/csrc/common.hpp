@@ -12,6 +12,8 @@
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t u16;
 
 #define CADENCE_DEV __device__ __forceinline__
@@ -44,6 +46,22 @@ CADENCE_DEV float sub_rn(float a, float b) { return __fsub_rn(a, b); }
 CADENCE_DEV float bmul(float a, float b) { return rbf(mul_rn(a, b)); }
 CADENCE_DEV float badd(float a, float b) { return rbf(add_rn(a, b)); }
 CADENCE_DEV float bsub(float a, float b) { return rbf(sub_rn(a, b)); }
+
+// Pairs: both values rounded by ONE v_cvt_pk_bf16_f32 (the same rounding as
+// two rbf calls), unpacked by a shift and a mask.
+CADENCE_DEV uint32_t pk2bf(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+CADENCE_DEV f32x2 rbf2(f32x2 v) {
+  const uint32_t w = pk2bf(v);
+  return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+CADENCE_DEV f32x2 bmul2(f32x2 a, f32x2 b) {
+  return rbf2(f32x2{mul_rn(a.x, b.x), mul_rn(a.y, b.y)});
+}
+CADENCE_DEV f32x2 badd2(f32x2 a, f32x2 b) {
+  return rbf2(f32x2{add_rn(a.x, b.x), add_rn(a.y, b.y)});
+}
 
 CADENCE_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 // Hardware transcendentals (v_exp_f32 / v_rcp_f32 / v_sqrt_f32, ~1-2 ulp in

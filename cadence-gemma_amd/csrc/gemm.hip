@@ -284,6 +284,82 @@ struct EpiRopeQKV {
   CADENCE_DEV void apply(int64_t, int, float, int) const {}
 };
 
+// Prefill q|k|v projection with RoPE in the staged epilogue (big engine,
+// one K split).  The weight rows are in qkv_rope_permutation order (as the
+// decode EpiRopeQKV): in the rotated half of a q / k head, columns 2i, 2i + 1
+// hold dims i, i + hd / 4, so every 8 staged columns carry 4 whole rotation
+// pairs and finish8 rotates them with rope_qkv_kernel's products, sums and
+// roundings (rounded GEMM output, bf16 sin / cos from the table) and writes
+// dims i0..i0+3 and i0 + hd/4.. as two 8-B rows; pass-through dims and the v
+// head are written as they are.  Outputs q [M][H*hd], k [M][hd], v [M][hd]
+// in natural dim order (modules.py:73-81, :430-436).
+struct EpiRopeQKVBig {
+  static constexpr bool kPaired = false;
+  static constexpr bool kStaged = true;
+  static constexpr bool kTile = false;
+  static constexpr bool kRowPref = true;
+  u16* q; u16* k; u16* v;
+  const int32_t* pos;
+  const u16* table; int table_len;
+  int H, hd;
+  struct RowPref { uint2 sn, cs; };
+  CADENCE_DEV float bias_at(bool, int, int) const { return 0.0f; }
+  CADENCE_DEV float stage(float x, float) const { return rbf(x); }
+  CADENCE_DEV int row_pos(int64_t m) const { return pos[m]; }
+  // the table entries of columns n..n+7's four rotation pairs (rotated
+  // columns inside the table only; the others read entry 0, unused)
+  CADENCE_DEV RowPref row_prefetch(int p, int n) const {
+    const int d = n % hd, quarter = hd / 4;
+    const bool ok = d < hd / 2 && p >= 0 && p < table_len;
+    const int64_t so = ok ? ((int64_t)p * 2) * quarter + (d >> 1) : 0;
+    return RowPref{*reinterpret_cast<const uint2*>(table + so),
+                   *reinterpret_cast<const uint2*>(table + so + (ok ? quarter : 0))};
+  }
+  CADENCE_DEV void finish8_pf(int64_t m, int n, uint4 v8, int p, const RowPref& pf) const {
+    const int h = n / hd, d = n % hd, half = hd / 2, quarter = hd / 4;
+    if (h > H) {
+      st16(v + m * hd + d, v8);
+      return;
+    }
+    u16* dst = h < H ? q + m * (int64_t)H * hd + (int64_t)h * hd : k + m * hd;
+    if (d >= half) {
+      st16(dst + d, v8);
+      return;
+    }
+    const int i0 = d >> 1;                  // pairs i0 .. i0 + 3
+    float sn[4], cs[4];
+    if (p >= 0 && p < table_len) {
+      const uint32_t sw[2] = {pf.sn.x, pf.sn.y}, cw[2] = {pf.cs.x, pf.cs.y};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sn[j] = __uint_as_float(j & 1 ? sw[j >> 1] & 0xffff0000u : sw[j >> 1] << 16);
+        cs[j] = __uint_as_float(j & 1 ? cw[j >> 1] & 0xffff0000u : cw[j >> 1] << 16);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rope_sincos(p, i0 + j, half, sn[j], cs[j]);
+    }
+    float x[8];
+    unpack8(v8, x);
+    uint32_t lo[2], hi[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float a0 = x[4 * j], b0 = x[4 * j + 1], a1 = x[4 * j + 2], b1 = x[4 * j + 3];
+      const int j0 = 2 * j, j1 = 2 * j + 1;
+      lo[j] = (uint32_t)f2bf(bsub(bmul(a0, cs[j0]), bmul(b0, sn[j0]))) |
+              ((uint32_t)f2bf(bsub(bmul(a1, cs[j1]), bmul(b1, sn[j1]))) << 16);
+      hi[j] = (uint32_t)f2bf(badd(bmul(b0, cs[j0]), bmul(a0, sn[j0]))) |
+              ((uint32_t)f2bf(badd(bmul(b1, cs[j1]), bmul(a1, sn[j1]))) << 16);
+    }
+    *reinterpret_cast<uint2*>(dst + i0) = make_uint2(lo[0], lo[1]);
+    *reinterpret_cast<uint2*>(dst + quarter + i0) = make_uint2(hi[0], hi[1]);
+  }
+  CADENCE_DEV void finish8(int64_t m, int n, uint4 v8, int g) const {
+    const int p = pos[m];
+    finish8_pf(m, n, v8, p, row_prefetch(p, n));
+  }
+};
+
 template <class E, class = void>
 struct EpiPairLanes { static constexpr bool value = false; };
 template <class E>
@@ -301,6 +377,17 @@ struct EpiPrefetch<E, std::void_t<decltype(E::kPrefetch)>> {
 
 // Decode GEMVs whose A operand may arrive unnormalised (the RMSNorm of the
 // producing residual projection applied on load, gemm_stream_kernel NORM).
+// Staged epilogues with per-row operands (kRowPref): the rolled finish loop
+// is unrolled and every iteration's row operands are loaded before the first
+// finish (row_pos for all rows, then row_prefetch for all), so the loop pays
+// two memory round trips in all instead of two per iteration.
+template <class E, class = void>
+struct EpiRowPref { static constexpr bool value = false; };
+template <class E>
+struct EpiRowPref<E, std::void_t<decltype(E::kRowPref)>> {
+  static constexpr bool value = E::kRowPref;
+};
+
 template <class E> struct EpiNormIn { static constexpr bool value = false; };
 
 struct EpiGatedGelu {
@@ -385,6 +472,24 @@ struct EpiRglruGates {
     const float mult = reset ? 1.0f : rbf(hw_sqrt(rbf(1.0f - a_sq)));
     av = reset ? 0.0f : a;
     nx = bmul(gated, mult);
+  }
+  // Two elements at once (the prefill gates kernel's channel pair): the
+  // same operations and rounding points as chain(), each rounding point one
+  // v_cvt_pk_bf16_f32 for both values; bit-identical to two chain() calls.
+  CADENCE_DEV void chain2(f32x2 gx_pre, f32x2 ga_pre, f32x2 xv, f32x2 sp, bool reset,
+                          f32x2& av, f32x2& nx) const {
+    const f32x2 gx = rbf2(f32x2{hw_sigmoid(gx_pre.x), hw_sigmoid(gx_pre.y)});
+    const f32x2 ga = rbf2(f32x2{hw_sigmoid(ga_pre.x), hw_sigmoid(ga_pre.y)});
+    const f32x2 log_a = bmul2(rbf2(f32x2{-8.0f * ga.x, -8.0f * ga.y}), sp);
+    const f32x2 a = rbf2(f32x2{hw_exp(log_a.x), hw_exp(log_a.y)});
+    const f32x2 l2 = rbf2(f32x2{2.0f * log_a.x, 2.0f * log_a.y});
+    const f32x2 a_sq = rbf2(f32x2{hw_exp(l2.x), hw_exp(l2.y)});
+    const f32x2 gated = bmul2(xv, gx);
+    const f32x2 om = rbf2(f32x2{sub_rn(1.0f, a_sq.x), sub_rn(1.0f, a_sq.y)});
+    const f32x2 mult = reset ? f32x2{1.0f, 1.0f}
+                             : rbf2(f32x2{hw_sqrt(om.x), hw_sqrt(om.y)});
+    av = reset ? f32x2{0.0f, 0.0f} : a;
+    nx = bmul2(gated, mult);
   }
   CADENCE_DEV void apply2(int64_t m, int j, float accx, float acca, int g) const {
     const int e = g * bw + j;
@@ -672,6 +777,25 @@ CADENCE_DEV void big_epilogue(const Epi& epi, f32x4 (&acc)[MR][4], u16* st, int 
     constexpr int RPI = 64 / CPRW;                 // rows per iteration
     const int obase = Epi::kPaired ? nbase / 2 : nbase;
     const int ch = lane % CPRW;
+    if constexpr (EpiRowPref<Epi>::value) {
+      constexpr int IT = MR * 16 / RPI;
+      const int col = obase + ch * 8;
+      int rp[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+        rp[it] = epi.row_pos(min(mbase + it * RPI + lane / CPRW, M - 1));
+      typename Epi::RowPref pf[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) pf[it] = epi.row_prefetch(rp[it], min(col, N - 8));
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int lr = it * RPI + lane / CPRW;
+        const int row = mbase + lr;
+        const uint4 v = *reinterpret_cast<const uint4*>(&st[lr * 64 + ((ch ^ (lr & 7)) << 3)]);
+        if (row < M && col < N) epi.finish8_pf(row, col, v, rp[it], pf[it]);
+      }
+      return;
+    }
 #pragma unroll 2
     for (int it = 0; it < MR * 16 / RPI; ++it) {
       const int lr = it * RPI + lane / CPRW;
@@ -1537,6 +1661,150 @@ __global__ __launch_bounds__(512) void gemm_gated_pipe_kernel(
   }
 }
 
+// Prefill RG-LRU gates (layers.py:321-365): both BlockDiagonalLinear GEMMs
+// of one head block g plus the gate chain, as a block-bound grouped GEMM.
+// K = BW is short (256 at 2B), so the block engine's per-tile prologue /
+// epilogue dominated it.  Here a workgroup is bound to one block g for its
+// whole life: its NW = BW / 32 waves each hold 64 of the block's 2 BW packed
+// output columns (32 x-gate + 32 a-gate rows of the same 32 channels, the
+// PackCache interleave) for all of K in registers, loaded once, and the
+// workgroup walks row tiles of 32 rows (t = blockIdx.x, + gridDim.x, ...).
+// The X tile (32 x BW bf16) is register-staged one tile ahead into the other
+// half of a double LDS buffer (XOR chunk swizzle on the row, so the
+// A-fragment ds_read_b128 of 16 rows is conflict-free); the chain's x operand
+// is read back from it.  The gate chain (seven transcendentals and fourteen
+// bf16 rounding points per element) is VALU-bound and sets the kernel's time;
+// each lane runs its two channels' chains as pairs (chain2: one
+// v_cvt_pk_bf16_f32 per rounding point of both).  Same MFMA k order as the
+// block engine (k-steps 0..BW/32-1 chained per accumulator), same rounding
+// points (EpiRglruGates::chain): bit-identical.
+template <int BW>
+__global__ __launch_bounds__(BW * 2) void rglru_gates_stream_kernel(
+    const u16* __restrict__ X, int64_t ldx, const u16* __restrict__ Wp, int M,
+    EpiRglruGates epi) {
+  constexpr int NW = BW / 32, KS = BW / 32, RT = 32, CPR = BW / 8;   // chunks per row
+  constexpr int RF = RT / 16;                                        // row fragments
+  constexpr int NT = NW * 64, LPT = RT * CPR / NT;                   // 16-B loads per thread
+  constexpr int SWM = CPR >= 16 ? 15 : CPR - 1;                      // chunk swizzle mask
+  static_assert(RT * CPR % NT == 0, "tile staging");
+  __shared__ uint4 xs[2][RT * CPR];
+  __shared__ int rs_[2][RT];
+  const int g = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ntiles = (M + RT - 1) / RT;
+  X += (int64_t)g * BW;
+  // this wave's weight fragments: tile j = 0, 1 x-gate rows (channels
+  // 32 wave + 16 j + lane % 16), j = 2, 3 a-gate rows of the same channels
+  const u16* wg = Wp + (int64_t)g * 2 * BW * BW;
+  uint4 wf[4][KS];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      wf[j][ks] = ld16(wg + (int64_t)(64 * wave + 16 * j + (lane & 15)) * BW + ks * 32 +
+                       8 * (lane >> 4));
+  // one use of every weight register before the loop (a never-true test on
+  // their XOR): the waitcnt pass then knows them landed, and the tile loop's
+  // MFMAs wait for nothing -- otherwise it counts the previous tile's stores
+  // down in front of them, every tile
+  {
+    uint32_t chk = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) chk ^= wf[j][ks].x ^ wf[j][ks].y ^ wf[j][ks].z ^ wf[j][ks].w;
+    if (chk == 0x6b43a9b5u && M < 0) epi.a_out[0] = 0;
+  }
+  // per-channel operands of the chain (constant over rows)
+  const int ch0 = 32 * wave + (lane & 15);
+  const int e0 = g * BW + ch0;
+  const f32x2 bx{bf2f(epi.bias_x[e0]), bf2f(epi.bias_x[e0 + 16])};
+  const f32x2 ba{bf2f(epi.bias_a[e0]), bf2f(epi.bias_a[e0 + 16])};
+  const f32x2 sp{bf2f(epi.softplus_a[e0]), bf2f(epi.softplus_a[e0 + 16])};
+  // register staging of one X tile: thread slot c -> (row c / CPR, chunk c %
+  // CPR), plus the tile's reset flags (thread c < RT: row c).  Branch-free:
+  // rows past M (and the tile after the last) read row M - 1, so a load
+  // never sits under a branch (that costs a vmcnt(0) at the join, i.e. the
+  // next tile's latency on this one's first MFMA).
+  uint4 st[LPT];
+  int sg;
+  auto fetch = [&](int t) {
+    t = min(t, ntiles - 1);
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = threadIdx.x + i * NT;
+      const int r = min(t * RT + c / CPR, M - 1);
+      st[i] = ld16(X + (int64_t)r * ldx + (c % CPR) * 8);
+    }
+    sg = epi.segpos[min(t * RT + (int)(threadIdx.x % RT), M - 1)];
+  };
+  auto stash = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = threadIdx.x + i * NT;
+      const int r = c / CPR, cc = c % CPR;
+      xs[b][r * CPR + (cc ^ (r & SWM))] = st[i];
+    }
+    if (threadIdx.x < RT) rs_[b][threadIdx.x] = sg == 0;
+  };
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  fetch(t);
+  stash(0);
+  int buf = 0;
+  for (; t < ntiles; t += gridDim.x) {
+    fetch(t + gridDim.x);                // lands while this tile computes
+    __syncthreads();                     // xs[buf] written by every thread
+    f32x4 acc[RF][4];
+#pragma unroll
+    for (int i = 0; i < RF; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 af[RF];
+#pragma unroll
+      for (int i = 0; i < RF; ++i) {
+        const int r = 16 * i + (lane & 15), cc = 4 * ks + (lane >> 4);
+        af[i] = __builtin_bit_cast(bf16x8, xs[buf][r * CPR + (cc ^ (r & SWM))]);
+      }
+#pragma unroll
+      for (int i = 0; i < RF; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              af[i], __builtin_bit_cast(bf16x8, wf[j][ks]), acc[i][j], 0, 0, 0);
+    }
+    // epilogue: lane holds rows 16 i + 4 (lane / 16) + r of channels ch0,
+    // ch0 + 16 (gx in tiles 0 / 1, ga in 2 / 3): one chain pair per row;
+    // rows past M recompute row M - 1 from its clamped copy and store the
+    // same values there (no store under a branch)
+    const u16* xl = reinterpret_cast<const u16*>(xs[buf]);
+#pragma unroll
+    for (int i = 0; i < RF; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = 16 * i + 4 * (lane >> 4) + r;
+        const int64_t m = min(t * RT + rl, M - 1);
+        const f32x2 xv{bf2f(xl[(rl * CPR + ((ch0 >> 3) ^ (rl & SWM))) * 8 + (ch0 & 7)]),
+                       bf2f(xl[(rl * CPR + (((ch0 + 16) >> 3) ^ (rl & SWM))) * 8 + (ch0 & 7)])};
+        f32x2 av, nx;
+        epi.chain2(badd2(rbf2(f32x2{acc[i][0][r], acc[i][1][r]}), bx),
+                   badd2(rbf2(f32x2{acc[i][2][r], acc[i][3][r]}), ba), xv, sp,
+                   rs_[buf][rl] != 0, av, nx);
+        u16* ap = epi.a_out + m * epi.ldo + e0;
+        u16* np = epi.nx_out + m * epi.ldo + e0;
+        const uint32_t ab = pk2bf(av), nb = pk2bf(nx);
+        ap[0] = (u16)ab;
+        ap[16] = (u16)(ab >> 16);
+        np[0] = (u16)nb;
+        np[16] = (u16)(nb >> 16);
+      }
+    buf ^= 1;
+    stash(buf);                          // the other buffer: last read a tile ago
+  }
+}
+
 // torch.argmax order: NaN beats every number, ties (and NaN vs NaN) go to
 // the lowest index -- a NaN row still yields an index inside the vocabulary
 CADENCE_DEV bool argmax_better(float ov, int oi, float v, int i) {
@@ -2220,11 +2488,11 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 12; }
+int cadence_abi_version(void) { return 13; }
 
 int cadence_gemm_set_engine(int engine) {
   const int prev = g_engine;
-  g_engine = engine;
+  if (engine >= 0) g_engine = engine;   // engine < 0: query only
   return prev;
 }
 
@@ -2336,6 +2604,41 @@ int cadence_qkv_rope_decode(const void* A, int64_t lda, const void* Wperm,
   launch_stream(static_cast<const u16*>(A), lda, static_cast<const u16*>(Wperm), ldw,
                 M, N, K, 1, 0, 0, epi, ksw, 1, nullptr, ldw == 0 ? 1 : 0,
                 static_cast<hipStream_t>(stream), nullptr, norm, norm_eps);
+  return (int)hipGetLastError();
+}
+
+int cadence_qkv_rope_prefill(const void* A, int64_t lda, const void* Wperm,
+                             int64_t ldw, const int32_t* positions, void* q_out,
+                             void* k_out, void* v_out, int64_t M, int64_t H, int64_t hd,
+                             int64_t K, const void* table, int64_t table_len,
+                             void* stream) {
+  if (M <= 0) return 0;
+  const int64_t N = (H + 2) * hd;
+  if (M <= kSkinnyMaxM || hd % 64 || H < 1 || K % BK || N % 64 || lda < K || ldw < K ||
+      !positions || big_splits(M, N, K, 1, big_tile_rows(M, N, K, 1)) > 1 ||
+      use_w4(N, K, big_tile_rows(M, N, K, 1)))
+    return (int)hipErrorInvalidValue;
+  const EpiRopeQKVBig epi{static_cast<u16*>(q_out), static_cast<u16*>(k_out),
+                          static_cast<u16*>(v_out), positions,
+                          static_cast<const u16*>(table), table ? (int)table_len : 0,
+                          (int)H, (int)hd};
+  const u16* a = static_cast<const u16*>(A);
+  const u16* w = static_cast<const u16*>(Wperm);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int rows = big_tile_rows(M, N, K, 1);
+  const int64_t bm = rows ? rows : 256;
+  const dim3 grid((unsigned)(((M + bm - 1) / bm) * ((N + 255) / 256)), 1);
+#define CADENCE_ROPE_BIG(P8_, MR_)                                                        \
+  hipLaunchKernelGGL((gemm_big_kernel<EpiRopeQKVBig, P8_, MR_>), grid, dim3(512), 0, st,  \
+                     a, lda, w, ldw, (int)M, (int)N, (int)K, (int64_t)0, (int64_t)0, epi)
+  switch (rows) {
+    case 160: CADENCE_ROPE_BIG(1, 5); break;
+    case 192: CADENCE_ROPE_BIG(1, 6); break;
+    case 224: CADENCE_ROPE_BIG(1, 7); break;
+    case 256: CADENCE_ROPE_BIG(1, 8); break;
+    default: CADENCE_ROPE_BIG(0, 8); break;
+  }
+#undef CADENCE_ROPE_BIG
   return (int)hipGetLastError();
 }
 
@@ -2464,10 +2767,33 @@ int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
                     static_cast<const u16*>(softplus_a), segment_pos,
                     static_cast<u16*>(a_out), static_cast<u16*>(nx_out), ldo,
                     (int)bw, nullptr, 0, nullptr, 0, nullptr, 0, 1};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // (lab switch: engine 0 keeps the block engine, for the bitwise A/B test)
+  if (g_engine != 0 && ldw == bw && M > 32 && (bw == 64 || bw == 128 || bw == 256) && ldx % 8 == 0 &&
+      ldo % 8 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0 &&
+      reinterpret_cast<uintptr_t>(Wpacked) % 16 == 0) {
+    // prefill: the block-bound streaming kernel, ~256 / heads workgroups per
+    // block (2 / 4 per CU for the narrower blocks' smaller waves counts)
+    const int64_t ntiles = (M + 31) / 32;
+    const int64_t per = std::max<int64_t>(1, (256 * (256 / bw)) / heads);
+    const dim3 grid((unsigned)std::min(ntiles, per), (unsigned)heads);
+    if (bw == 256)
+      hipLaunchKernelGGL(rglru_gates_stream_kernel<256>, grid, dim3(512), 0, st,
+                         static_cast<const u16*>(X), ldx, static_cast<const u16*>(Wpacked),
+                         (int)M, epi);
+    else if (bw == 128)
+      hipLaunchKernelGGL(rglru_gates_stream_kernel<128>, grid, dim3(256), 0, st,
+                         static_cast<const u16*>(X), ldx, static_cast<const u16*>(Wpacked),
+                         (int)M, epi);
+    else
+      hipLaunchKernelGGL(rglru_gates_stream_kernel<64>, grid, dim3(128), 0, st,
+                         static_cast<const u16*>(X), ldx, static_cast<const u16*>(Wpacked),
+                         (int)M, epi);
+    return (int)hipGetLastError();
+  }
   return launch_gemm(static_cast<const u16*>(X), ldx,
                      static_cast<const u16*>(Wpacked), ldw, M, 2 * bw, bw, heads,
-                     bw, 2 * bw * bw, epi, workspace, ws_bytes,
-                     static_cast<hipStream_t>(stream));
+                     bw, 2 * bw * bw, epi, workspace, ws_bytes, st);
 }
 
 int cadence_rglru_step(const void* X, int64_t ldx, const void* Wpacked,

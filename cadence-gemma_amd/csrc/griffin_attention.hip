@@ -39,8 +39,6 @@
 
 namespace {
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef const void __attribute__((address_space(1)))* ga_gptr_t;
 typedef void __attribute__((address_space(3)))* ga_lptr_t;

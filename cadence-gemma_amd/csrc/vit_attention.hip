@@ -24,7 +24,6 @@
 namespace {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 // max of scores that are finite or -inf.  Compiler-visible (not inline
 // asm): the hazard recognizer must see these reads of fresh MFMA results

@@ -94,8 +94,9 @@ int cadence_gemm_engine(int64_t M, int64_t N, int64_t K, int64_t groups);
 
 /* Lab A/B switch of the prefill engine: 1 (default) = the shipped plan (the
  * 4-wave gemm_w4_kernel for K >= 2048 on 224 / 256-row tile plans, else the
- * 8-wave gemm_big_kernel), 0 = 8-wave only; returns the previous value.
- * Host state only. */
+ * 8-wave gemm_big_kernel; prefill RG-LRU gates of 64 / 128 / 256-wide blocks
+ * on rglru_gates_stream_kernel), 0 = 8-wave block engine only; a negative
+ * value only queries.  Returns the previous value.  Host state only. */
 int cadence_gemm_set_engine(int engine);
 
 /* ---- GEMMs with fused epilogues ---------------------------------------- */
@@ -340,6 +341,22 @@ int cadence_qkv_rope_decode(const void* A, int64_t lda, const void* Wperm,
                             int64_t hd, int64_t K, const void* table,
                             int64_t table_len, int norm, float norm_eps,
                             void* stream);
+
+/* Prefill (M > 64 rows) q|k|v projection with RoPE in the GEMM epilogue
+ * (replaces cadence_gemm_linear + cadence_rope_qkv of the prompt pass;
+ * reference modules.py:429-440 proj_q/k/v + apply_rope, :53-87): the block
+ * engine with Wperm in cadence_qkv_rope_decode's row order, each 8 staged
+ * output columns (4 rotation pairs) rotated and written to q [M][H*hd],
+ * k [M][hd], v [M][hd] in natural dim order, with cadence_rope_qkv's
+ * products and roundings.  Row-major A and Wperm (lda, ldw >= K); hd % 64
+ * == 0, K % 64 == 0.  Returns hipErrorInvalidValue for a shape whose plan is
+ * not one unsplit block-engine launch (small M: split K, or the 4-wave
+ * engine); the caller then runs the two-launch form. */
+int cadence_qkv_rope_prefill(const void* A, int64_t lda, const void* Wperm,
+                             int64_t ldw, const int32_t* positions, void* q_out,
+                             void* k_out, void* v_out, int64_t M, int64_t H, int64_t hd,
+                             int64_t K, const void* table, int64_t table_len,
+                             void* stream);
 
 /* sin / cos table for cadence_rope_qkv: table[p][0][i] = bf16(sin(p * f_i)),
  * table[p][1][i] = bf16(cos(p * f_i)), i < hd / 4, f_i as modules.py:73-77

@@ -250,6 +250,40 @@ def test_decode_packed_rglru_gates_bitwise(dev):
   assert torch.equal(a1, a2) and torch.equal(x1, x2)
 
 
+@pytest.mark.parametrize("m,h,bw", [(10208, 10, 256), (319, 10, 256), (33, 10, 256),
+                                    (100, 4, 128), (77, 2, 64), (4096, 8, 128)])
+def test_prefill_rglru_gates_stream_kernel_bitwise(dev, m, h, bw):
+  """The prefill gates kernel (rglru_gates_stream_kernel: block-bound
+  workgroups, weights in registers, 32-row tiles) against the block engine
+  it replaced (lab switch engine 0), bitwise: same MFMA k order, same
+  chain.  Resets, a ragged last tile, every block width it takes, and the
+  bench shape (32 x 319 rows)."""
+  from cadence import _lib
+  g = torch.Generator().manual_seed(31)
+  e = h * bw
+  x = rnd(m, 2 * e, gen=g).to(dev)[:, e:]          # strided: the y|x GEMM output
+  w = rnd(h, 2 * bw, bw, scale=1 / math.sqrt(bw), gen=g).to(dev)
+  bx, ba = rnd(e, scale=0.3, gen=g).to(dev), rnd(e, scale=0.3, gen=g).to(dev)
+  sp = torch.rand(e, generator=g).to(BF).to(dev)
+  pos = torch.randint(0, 5, (m,), generator=g, dtype=torch.int32).to(dev)
+  lib = _lib.load()
+  a1, x1 = ops.ops.rglru_gates(x, w, bx, ba, sp, pos)
+  prev = lib.cadence_gemm_set_engine(0)
+  try:
+    a0, x0 = ops.ops.rglru_gates(x, w, bx, ba, sp, pos)
+  finally:
+    lib.cadence_gemm_set_engine(prev)
+  if m > 64 and lib.cadence_gemm_big_splits(m, 2 * bw, bw, h) == 1:
+    assert torch.equal(a1, a0) and torch.equal(x1, x0)
+  else:
+    # for this small M the old path split K (the skinny engine's wave
+    # partials at M <= 64, or split-K partials) and summed in another
+    # order: the unsplit chain rounds a few sums differently
+    assert_close_bf16(a1, a0, rtol=1e-2, atol=1e-2, min_equal=0.99, what="a")
+    assert_close_bf16(x1, x0, rtol=1e-2, atol=1e-2, min_equal=0.99, what="nx")
+  assert bool((a1[pos == 0] == 0).all())
+
+
 @pytest.mark.parametrize("packed", [False, True])
 def test_rglru_step_matches_gates_then_scan(dev, packed):
   """Fused decode step == gate chain then rnn_scan's T == 1 branch, bitwise,
@@ -394,6 +428,32 @@ def test_rope_and_local_attention(dev, b, t, h, hd, window, split):
   got = got.view(b, t, h, hd)
   assert_close_bf16(got, want, rtol=3e-2, atol=3e-2, what="local attention")
   assert rel_l2(got, want) < 1e-2
+
+
+@pytest.mark.parametrize("m,h,hd,k", [(32 * 319, 10, 256, 2560), (32 * 639, 10, 256, 2560),
+                                      (300, 4, 128, 512), (1000, 6, 64, 512)])
+def test_qkv_rope_prefill_matches_two_launch_form(dev, m, h, hd, k):
+  """Prompt-pass q|k|v GEMM with RoPE in the staged epilogue (permuted
+  weight rows) == linear on the natural rows, then rope_qkv: bitwise (same
+  per-column MFMA chains, same rotation arithmetic).  Positions include
+  document resets, -1 padding and positions past the sin / cos table."""
+  if not ops.qkv_rope_prefill_ok(m, h, hd, k):
+    pytest.skip("plan is not one unsplit block-engine launch")
+  g = torch.Generator().manual_seed(21)
+  x = rnd(m, k, gen=g).to(dev)
+  w = rnd((h + 2) * hd, k, scale=1 / math.sqrt(k), gen=g).to(dev)
+  pos = torch.randint(-1, 3000, (m,), generator=g, dtype=torch.int32)
+  pos[::7] = 0
+  pos[5] = ops.ROPE_TABLE_POSITIONS + 17
+  pos = pos.to(dev)
+  table = ops.rope_table(dev, hd)
+  qkv = ops.linear(x, w)
+  q0, k0, v0 = ops.ops.rope_qkv(qkv, pos, h, hd, table)
+  wp = w[ops.qkv_rope_permutation(h, hd, dev)].contiguous()
+  q1, k1, v1 = ops.ops.qkv_rope_prefill(x, wp, pos, h, hd, table)
+  assert torch.equal(v1, v0)
+  assert torch.equal(k1, k0)
+  assert torch.equal(q1, q0)
 
 
 @pytest.mark.parametrize("b,ctx", [(32, 352), (1, 1500), (2, 2100), (4, 0)])

@@ -1,10 +1,12 @@
-"""RG-LRU gate GEMM microbenchmark (prefill shape, M = 32 x 319 rows):
-the fused gate chain vs plain GEMMs of the same operand shapes."""
+"""RG-LRU prefill gates microbenchmark (bench shape, M = 32 x 319 rows,
+E = 2560, 10 blocks of 256): rglru_gates_stream_kernel (engine 1) against
+the block engine it replaced (engine 0), HIP events around 20 launches;
+HBM bytes = x in + a, normalised x out (+ the 2.6 MB of packed weights)."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cadence-gemma_amd"), ROOT]
 import torch
-from cadence import ops
+from cadence import _lib, ops
 
 BF = torch.bfloat16
 
@@ -21,25 +23,22 @@ def timeit(fn, reps=20):
 
 def main():
   dev = torch.device("cuda")
-  M = int(os.environ.get("M", str(32 * 319)))
-  E, H, bw = 2560, 10, 256
-  x = torch.randn(M, E, device=dev).to(BF)
-  wg = (torch.randn(H, 2 * bw, bw, device=dev) / 16).to(BF)
-  bx = torch.zeros(E, dtype=BF, device=dev)
-  pos = torch.ones(M, dtype=torch.int32, device=dev)
-  w1 = wg[0].contiguous()
-  wbig = torch.randn(5120, 256, device=dev).to(BF)
-  xs = x[:, :256]
-  cases = [
-      ("rglru_gates (10 groups)", lambda: ops.ops.rglru_gates(x, wg, bx, bx, bx, pos)),
-      ("linear N=512 K=256 x10", lambda: [ops.linear(xs, w1) for _ in range(10)]),
-      ("linear N=5120 K=256", lambda: ops.linear(xs, wbig)),
-      ("linear N=5120 K=2560", lambda: ops.linear(x, wx)),
-  ]
-  global wx
-  wx = torch.randn(5120, 2560, device=dev).to(BF)
-  for name, fn in cases:
-    print(f"{name:28s} {timeit(fn):9.1f} us", flush=True)
+  lib = _lib.load()
+  for M in (32 * 319, 319, 8 * 2048):
+    E, H, bw = 2560, 10, 256
+    yx = torch.randn(M, 2 * E, device=dev).to(BF)
+    x = yx[:, E:]
+    wg = (torch.randn(H, 2 * bw, bw, device=dev) / 16).to(BF)
+    bx = torch.zeros(E, dtype=BF, device=dev)
+    sp = torch.rand(E, device=dev).to(BF)
+    pos = torch.randint(0, 50, (M,), dtype=torch.int32, device=dev)
+    nbytes = 3 * M * E * 2 + wg.numel() * 2
+    for eng in (1, 0):
+      prev = lib.cadence_gemm_set_engine(eng)
+      us = timeit(lambda: ops.ops.rglru_gates(x, wg, bx, bx, sp, pos))
+      lib.cadence_gemm_set_engine(prev)
+      print(f"M={M:6d} engine {eng}: {us:8.2f} us  {nbytes / us / 1e3:7.1f} GB/s "
+            f"({nbytes / us / 1e3 / 8000:.3f} of 8 TB/s)", flush=True)
 
 
 if __name__ == "__main__":
