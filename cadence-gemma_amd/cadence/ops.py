@@ -540,7 +540,7 @@ def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos,
       _s(x)), "rglru_gates")
   if ev is not None:
     if (not decode_layout and bw in (64, 128, 256) and
-        _lib.load().cadence_gemm_set_engine(-1) != 0):
+        _lib.load().cadence_gemm_set_engine(-1) & 2):
       # the block-bound streaming kernel: priced on HBM bytes (x in, a and
       # normalised x out, the packed weights once)
       TIMER.stop(ev, f"rglru_gates_stream_kernel<{bw}>",

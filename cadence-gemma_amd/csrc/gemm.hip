@@ -2237,7 +2237,10 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
                               splits, parts, packed, st, counters, 0.0f);
 }
 
-int g_engine = 1;   // lab A/B switch of the prefill engine (0 = 8-wave only)
+// lab A/B switch of the prefill engines, a bit mask: bit 0 = the 4-wave
+// gemm_w4_kernel on its plans, bit 1 = rglru_gates_stream_kernel (0 = the
+// 8-wave block engine for everything)
+int g_engine = 3;
 
 // The 4-wave engine runs the wide long-K GEMMs (the gated MLP up-projection,
 // N = 2F = 15360, K = 2560) on 224 / 256-row tile plans.  Measured A/B in
@@ -2251,7 +2254,7 @@ int g_engine = 1;   // lab A/B switch of the prefill engine (0 = 8-wave only)
 // Short K keeps the 8-wave engine, whose 8 waves also finish element-wise
 // epilogues twice as fast (fc1's erf-GELU at K = 1024: 0.87x on 4 waves).
 bool use_w4(int64_t N, int64_t K, int rows) {
-  return g_engine != 0 && K >= 2048 && N >= 8192 && (rows == 224 || rows == 256);
+  return (g_engine & 1) && K >= 2048 && N >= 8192 && (rows == 224 || rows == 256);
 }
 
 // Prefill engine plan for M > kSkinnyMaxM: 0 = 2-buffer 256-row kernel,
@@ -2769,7 +2772,7 @@ int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
                     (int)bw, nullptr, 0, nullptr, 0, nullptr, 0, 1};
   hipStream_t st = static_cast<hipStream_t>(stream);
   // (lab switch: engine 0 keeps the block engine, for the bitwise A/B test)
-  if (g_engine != 0 && ldw == bw && M > 32 && (bw == 64 || bw == 128 || bw == 256) && ldx % 8 == 0 &&
+  if ((g_engine & 2) && ldw == bw && M > 32 && (bw == 64 || bw == 128 || bw == 256) && ldx % 8 == 0 &&
       ldo % 8 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0 &&
       reinterpret_cast<uintptr_t>(Wpacked) % 16 == 0) {
     // prefill: the block-bound streaming kernel, ~256 / heads workgroups per

@@ -313,24 +313,27 @@ __global__ __launch_bounds__(GA_MAXW * 64) void griffin_attn_kernel(GAArgs a) {
 // zero Q fragment, or landing in output dims that are not stored.  fp32
 // scores (the reference tower is fp32); only the tail tile is masked.
 
-template <int KS, int NDT, int CPR, int NB>
-__global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
+template <int KS, int NDT, int CPR, int NB, int NW, int QT>
+__global__ __launch_bounds__(NW * 64, 2) void vit_stream_attn_kernel(
     const u16* __restrict__ qkv, u16* __restrict__ out, int N, int H, int hd,
     float scale_log2) {
   // CPR 16-B chunks per LDS row: 8 (128 B) for hd 64, 16 (256 B) for hd 72;
-  // NB tile buffers (tile t + NB - 1 is fetched while tile t is computed)
+  // NB tile buffers (tile t + NB - 1 is fetched while tile t is computed);
+  // NW waves per workgroup, QT 16-query tiles per wave: every K fragment and
+  // V^T fragment a wave reads from LDS feeds QT query tiles' MFMAs (the LDS
+  // reads of shared K / V^T, 8 waves x 16 queries per tile, bounded the
+  // QT = 1 form, not the MFMA pipe)
   constexpr int TILE = GA_KT * CPR;   // uint4 per K or V image
   constexpr int NP = TILE / 64;       // 1-KiB DMA pieces per image
-  constexpr int NW = 8;
   constexpr int DPW = 2 * NP / NW;    // DMA instructions per wave per tile
   constexpr int RPP = 64 / CPR;       // rows per DMA piece
   static_assert(4 * KS <= CPR && 2 * NDT <= CPR && 2 * NP % NW == 0, "row padding");
-  static_assert(NB == 2 || (NB == 3 && DPW == 2), "vmcnt below");
+  static_assert(NB == 2 || (NB == 3 && (DPW == 2 || DPW == 4)), "vmcnt below");
   __shared__ __attribute__((aligned(16))) uint4 smem[NB * 2 * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int nqb = (N + NW * 16 - 1) / (NW * 16);
+  const int nqb = (N + NW * 16 * QT - 1) / (NW * 16 * QT);
   int b, h, qb;
   {
     const int total = gridDim.x, lin = blockIdx.x;
@@ -369,24 +372,34 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
   };
   const int ntiles = (N + GA_KT - 1) / GA_KT;
 
-  const int q0 = (qb * NW + wave) * 16;
-  const int qi = min(q0 + c16, N - 1);
-  bf16x8 qf[KS];
+  // this wave's query tiles u: queries q0[u] .. q0[u] + 15
+  int q0[QT];
+  bf16x8 qf[QT][KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    const int d = ks * 32 + 8 * g;
-    qf[ks] = __builtin_bit_cast(bf16x8, d < hd ? ld16(base + qi * rs + d)
-                                               : make_uint4(0, 0, 0, 0));
+  for (int u = 0; u < QT; ++u) {
+    q0[u] = ((qb * NW + wave) * QT + u) * 16;
+    const int qi = min(q0[u] + c16, N - 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int d = ks * 32 + 8 * g;
+      qf[u][ks] = __builtin_bit_cast(bf16x8, d < hd ? ld16(base + qi * rs + d)
+                                                    : make_uint4(0, 0, 0, 0));
+    }
   }
   // q in registers before any DMA is issued, by a wait the compiler sees
   // (otherwise it keeps the q loads pending and puts a vmcnt(0) -- a wait
   // for every tile in flight -- before each tile's first MFMA)
   __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
   for (int t = 0; t < NB - 1 && t < ntiles; ++t) stage(t, t);
-  f32x4 o[NDT];
+  f32x4 o[QT][NDT];
+  float m[QT], l[QT];
 #pragma unroll
-  for (int j = 0; j < NDT; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.0f;
+  for (int u = 0; u < QT; ++u) {
+#pragma unroll
+    for (int j = 0; j < NDT; ++j) o[u][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m[u] = -INFINITY;
+    l[u] = 0.0f;
+  }
   constexpr float kThr = 8.0f;
   const int tq = c16 >> 2, tp = c16 & 3;
 
@@ -394,8 +407,12 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
     const int buf = t % NB;
     // tile t landed (this wave's DMA: tiles > t may stay in flight), then
     // every wave's: raw s_barrier (__syncthreads would drain all DMA)
-    if (NB == 3 && t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (NB == 3 && t + 1 < ntiles) {
+      if constexpr (DPW == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -415,64 +432,68 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
         kf[tt][ks] = __builtin_bit_cast(bf16x8, kimg[kr * CPR + ((4 * ks + g) ^ (kr & (CPR - 1)))]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    f32x4 s[4];
+    bf16x8 pf[QT][2];
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
-      s[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < QT; ++u) {
+      f32x4 s[4];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-        s[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[tt][ks], qf[ks], s[tt], 0, 0, 0);
-    }
-    if (c0 + GA_KT > N) {              // tail tile: keys past N
+      for (int tt = 0; tt < 4; ++tt) {
+        s[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int tt = 0; tt < 4; ++tt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (c0 + 16 * tt + 4 * g + r >= N) s[tt][r] = -INFINITY;
-    }
-    float smax = ga_max3(s[0][0], s[0][1], s[0][2]);
-    smax = ga_max3(smax, s[0][3], s[1][0]);
-    smax = ga_max3(smax, s[1][1], s[1][2]);
-    smax = ga_max3(smax, s[1][3], s[2][0]);
-    smax = ga_max3(smax, s[2][1], s[2][2]);
-    smax = ga_max3(smax, s[2][3], s[3][0]);
-    smax = ga_max3(smax, s[3][1], s[3][2]);
-    smax = ga_max2(smax, s[3][3]);
-    smax = ga_max_rows(smax);
-    const float mt = smax * scale_log2;
-    const bool need = mt > m + kThr;
-    if (__any(need)) {
-      const float mn = need ? mt : m;
-      const float alpha = need ? __builtin_amdgcn_exp2f(m - mn) : 1.0f;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[dt][r] *= alpha;
-      l *= alpha;
-      m = mn;
-    }
-    const float nm = -m;               // every query has a key in tile 0
-    bf16x8 pf[2];
-    float ps0 = 0.0f, ps1 = 0.0f;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      uint32_t pk[4];
-#pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        const int tt = 2 * kk + (j >> 2), r = j & 3;
-        const float e0 = __builtin_amdgcn_exp2f(fmaf(s[tt][r], scale_log2, nm));
-        const float e1 = __builtin_amdgcn_exp2f(fmaf(s[tt][r + 1], scale_log2, nm));
-        ps0 += e0;
-        ps1 += e1;
-        pk[j >> 1] = ga_pk2bf(f32x2{e0, e1});
+        for (int ks = 0; ks < KS; ++ks)
+          s[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[tt][ks], qf[u][ks], s[tt], 0, 0, 0);
       }
-      pf[kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+      if (c0 + GA_KT > N) {              // tail tile: keys past N
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (c0 + 16 * tt + 4 * g + r >= N) s[tt][r] = -INFINITY;
+      }
+      float smax = ga_max3(s[0][0], s[0][1], s[0][2]);
+      smax = ga_max3(smax, s[0][3], s[1][0]);
+      smax = ga_max3(smax, s[1][1], s[1][2]);
+      smax = ga_max3(smax, s[1][3], s[2][0]);
+      smax = ga_max3(smax, s[2][1], s[2][2]);
+      smax = ga_max3(smax, s[2][3], s[3][0]);
+      smax = ga_max3(smax, s[3][1], s[3][2]);
+      smax = ga_max2(smax, s[3][3]);
+      smax = ga_max_rows(smax);
+      const float mt = smax * scale_log2;
+      const bool need = mt > m[u] + kThr;
+      if (__any(need)) {
+        const float mn = need ? mt : m[u];
+        const float alpha = need ? __builtin_amdgcn_exp2f(m[u] - mn) : 1.0f;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[u][dt][r] *= alpha;
+        l[u] *= alpha;
+        m[u] = mn;
+      }
+      const float nm = -m[u];            // every query has a key in tile 0
+      float ps0 = 0.0f, ps1 = 0.0f;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        uint32_t pk[4];
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const int tt = 2 * kk + (j >> 2), r = j & 3;
+          const float e0 = __builtin_amdgcn_exp2f(fmaf(s[tt][r], scale_log2, nm));
+          const float e1 = __builtin_amdgcn_exp2f(fmaf(s[tt][r + 1], scale_log2, nm));
+          ps0 += e0;
+          ps1 += e1;
+          pk[j >> 1] = ga_pk2bf(f32x2{e0, e1});
+        }
+        pf[u][kk] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+      }
+      l[u] += ps0 + ps1;
     }
-    l += ps0 + ps1;
     // V^T fragments by the transposing LDS read: all 2 NDT of a key half in
     // ONE asm statement with one lgkmcnt wait (the compiler's builtin for the
     // read is preceded by a vmcnt(0), i.e. it would wait for the next tile's
-    // DMA; a statement per pair waited once per pair)
+    // DMA; a statement per pair waited once per pair), each fragment feeding
+    // the QT query tiles' P.V MFMAs
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int r1 = 32 * kk + 4 * g + tq, r2 = r1 + 16;
@@ -518,23 +539,28 @@ __global__ __launch_bounds__(512, 2) void vit_stream_attn_kernel(
       for (int dt = 0; dt < NDT; ++dt) {
         const bf16x8 vf = __builtin_bit_cast(
             bf16x8, make_uint4(w[2 * dt].x, w[2 * dt].y, w[2 * dt + 1].x, w[2 * dt + 1].y));
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[kk], o[dt], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < QT; ++u)
+          o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[u][kk], o[u][dt], 0, 0, 0);
       }
     }
   }
-  float lt = l;
-  lt += __shfl_xor(lt, 16, 64);
-  lt += __shfl_xor(lt, 32, 64);
-  const float inv = 1.0f / lt;
-  if (q0 + c16 < N) {
-    u16* orow = out + ((int64_t)b * N + q0 + c16) * D + (int64_t)h * hd;
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-      const int d0 = dt * 16 + 4 * g;
-      if (d0 < hd) {
-        const uint32_t lo2 = ga_pk2bf(f32x2{o[dt][0] * inv, o[dt][1] * inv});
-        const uint32_t hi2 = ga_pk2bf(f32x2{o[dt][2] * inv, o[dt][3] * inv});
-        *reinterpret_cast<uint2*>(orow + d0) = make_uint2(lo2, hi2);
+  for (int u = 0; u < QT; ++u) {
+    float lt = l[u];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const float inv = 1.0f / lt;
+    if (q0[u] + c16 < N) {
+      u16* orow = out + ((int64_t)b * N + q0[u] + c16) * D + (int64_t)h * hd;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const int d0 = dt * 16 + 4 * g;
+        if (d0 < hd) {
+          const uint32_t lo2 = ga_pk2bf(f32x2{o[u][dt][0] * inv, o[u][dt][1] * inv});
+          const uint32_t hi2 = ga_pk2bf(f32x2{o[u][dt][2] * inv, o[u][dt][3] * inv});
+          *reinterpret_cast<uint2*>(orow + d0) = make_uint2(lo2, hi2);
+        }
       }
     }
   }
@@ -568,17 +594,23 @@ __attribute__((visibility("hidden"))) int vit_stream_attention_launch(
     void* stream) {
   if ((hd != 64 && hd != 72) || N < 1) return -1;
   if (((uintptr_t)qkv | (uintptr_t)out) % 16) return -1;
-  const int64_t nqb = (N + 127) / 128;
-  const dim3 grid((unsigned)(B * H * nqb)), block(512);
+  // 8 waves x 1 query tile (128 queries) per workgroup, two per CU.  4 x 2
+  // (each K / V^T fragment read from LDS feeding two query tiles: half the
+  // LDS reads) measured slower: DINO 336 px 91.5 -> 99.8 us, SigLIP 98 -> 118
+  // (profiles/r03o_vit_stream_qt2.log) -- the tile loop is latency-bound,
+  // and 2 query tiles per wave cost occupancy
+  constexpr int NWQ = 8, QTQ = 1;
+  const int64_t nqb = (N + NWQ * 16 * QTQ - 1) / (NWQ * 16 * QTQ);
+  const dim3 grid((unsigned)(B * H * nqb)), block(NWQ * 64);
   const float sl2 = 1.4426950408889634f / sqrtf((float)hd);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const u16* in = static_cast<const u16*>(qkv);
   u16* o = static_cast<u16*>(out);
   if (hd == 64)
-    hipLaunchKernelGGL((vit_stream_attn_kernel<2, 4, 8, 3>), grid, block, 0, st, in, o,
-                       (int)N, (int)H, (int)hd, sl2);
+    hipLaunchKernelGGL((vit_stream_attn_kernel<2, 4, 8, 3, NWQ, QTQ>), grid, block, 0, st, in,
+                       o, (int)N, (int)H, (int)hd, sl2);
   else
-    hipLaunchKernelGGL((vit_stream_attn_kernel<3, 5, 16, 2>), grid, block, 0, st, in, o,
-                       (int)N, (int)H, (int)hd, sl2);
+    hipLaunchKernelGGL((vit_stream_attn_kernel<3, 5, 16, 2, NWQ, QTQ>), grid, block, 0, st,
+                       in, o, (int)N, (int)H, (int)hd, sl2);
   return (int)hipGetLastError();
 }

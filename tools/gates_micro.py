@@ -33,7 +33,7 @@ def main():
     sp = torch.rand(E, device=dev).to(BF)
     pos = torch.randint(0, 50, (M,), dtype=torch.int32, device=dev)
     nbytes = 3 * M * E * 2 + wg.numel() * 2
-    for eng in (1, 0):
+    for eng in (3, 0):
       prev = lib.cadence_gemm_set_engine(eng)
       us = timeit(lambda: ops.ops.rglru_gates(x, wg, bx, bx, sp, pos))
       lib.cadence_gemm_set_engine(prev)

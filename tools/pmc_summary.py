@@ -23,6 +23,13 @@ KEYS = {
         r"gemm_big_kernel<[^>]*EpiGatedGelu, 1, 7>",
         2 * (10208 * 2560 + 2 * 7680 * 2560 + 10208 * 7680),
         "A (M x K) + W (2F x K) + out (M x F), bf16"),
+    "gemm_w4_kernel<EpiGatedGelu, 7>": (
+        r"gemm_w4_kernel<[^>]*EpiGatedGelu, 7>",
+        2 * (10208 * 2560 + 2 * 7680 * 2560 + 10208 * 7680),
+        "A (M x K) + W (2F x K) + out (M x F), bf16"),
+    "rglru_gates_stream_kernel<256>": (
+        r"rglru_gates_stream_kernel<256>", 3 * 10208 * 2560 * 2 + 10 * 512 * 256 * 2,
+        "x in + a, normalised x out (bf16) + packed gate weights"),
     "gemm_gated_pipe_kernel<10, 2, 3, true> (decode)": (
         r"gemm_gated_pipe_kernel<10, 2, 3, true>", 79134720,
         "2F x K bf16 weights + activations + out"),
