@@ -594,23 +594,21 @@ __attribute__((visibility("hidden"))) int vit_stream_attention_launch(
     void* stream) {
   if ((hd != 64 && hd != 72) || N < 1) return -1;
   if (((uintptr_t)qkv | (uintptr_t)out) % 16) return -1;
-  // 8 waves x 1 query tile (128 queries) per workgroup, two per CU.  4 x 2
-  // (each K / V^T fragment read from LDS feeding two query tiles: half the
-  // LDS reads) measured slower: DINO 336 px 91.5 -> 99.8 us, SigLIP 98 -> 118
-  // (profiles/r03o_vit_stream_qt2.log) -- the tile loop is latency-bound,
-  // and 2 query tiles per wave cost occupancy
-  constexpr int NWQ = 8, QTQ = 1;
-  const int64_t nqb = (N + NWQ * 16 * QTQ - 1) / (NWQ * 16 * QTQ);
-  const dim3 grid((unsigned)(B * H * nqb)), block(NWQ * 64);
+  // 128 queries per workgroup: hd 64 as 4 waves x 2 query tiles (each K /
+  // V^T fragment read from LDS feeds two tiles' MFMAs), hd 72 as 8 waves x
+  // 1 tile.  Same-box A/B (profiles/r03q_vit_stream_qt_ab.log): hd 64
+  // 4 x 2 is 3-8 % faster at 336 / 384 px, hd 72 the same or slower.
   const float sl2 = 1.4426950408889634f / sqrtf((float)hd);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const u16* in = static_cast<const u16*>(qkv);
   u16* o = static_cast<u16*>(out);
+  const int64_t nqb = (N + 127) / 128;
+  const dim3 grid((unsigned)(B * H * nqb));
   if (hd == 64)
-    hipLaunchKernelGGL((vit_stream_attn_kernel<2, 4, 8, 3, NWQ, QTQ>), grid, block, 0, st, in,
+    hipLaunchKernelGGL((vit_stream_attn_kernel<2, 4, 8, 3, 4, 2>), grid, dim3(256), 0, st, in,
                        o, (int)N, (int)H, (int)hd, sl2);
   else
-    hipLaunchKernelGGL((vit_stream_attn_kernel<3, 5, 16, 2, NWQ, QTQ>), grid, block, 0, st,
+    hipLaunchKernelGGL((vit_stream_attn_kernel<3, 5, 16, 2, 8, 1>), grid, dim3(512), 0, st,
                        in, o, (int)N, (int)H, (int)hd, sl2);
   return (int)hipGetLastError();
 }
