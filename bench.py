@@ -353,7 +353,8 @@ def main():
       args.batch, 1)
 
   def step(events=None, pipeline=True):
-    if args.decode and pipeline and not args.no_pipeline:
+    # (one micro-batch has nothing to overlap: plain Sampler.generate)
+    if args.decode and pipeline and not args.no_pipeline and n_micro > 1:
       # micro-batch j + 1's prefill overlaps micro-batch j's decode
       # (Sampler.generate_many); `events` time the last micro-batch
       sts = sampler.generate_many(
@@ -425,10 +426,17 @@ def main():
     # ~3 % of the step); a second pass of the same K steps times the kernels
     dt, step_ev, ev_list, out = timed_pass(False)
     ksum = {}
+    pipelined = bool(args.decode and not args.no_pipeline and n_micro > 1)
     if not args.no_kernel_timing:
-      # prefill / decode-step events from the sequential pass as well
-      _, _, ev_list, _ = timed_pass(True)
+      _, _, ev_seq, _ = timed_pass(True)
       ksum = ops.TIMER.summary()
+      # with two lanes in flight the headline pass's prefill / decode event
+      # pairs would time queueing behind the other lane: take them from the
+      # sequential pass then (otherwise from the headline pass, which carries
+      # no per-kernel events: a B = 1 prefill is launch-bound, and the
+      # events would inflate it)
+      if pipelined:
+        ev_list = ev_seq
   elapsed = D.max_over_ranks(dt)
   per_step = sorted(step_ev[i].elapsed_time(step_ev[i + 1])
                     for i in range(args.steps))
@@ -513,16 +521,17 @@ def main():
             "prompt_len": args.prompt, "decode_steps": args.decode,
             "seq_len": n_vis + args.prompt + args.decode,
             "parallelism": f"dp{world}",
-            "micro_batch_pipeline": bool(args.decode and not args.no_pipeline),
+            "micro_batch_pipeline": bool(args.decode and not args.no_pipeline
+                                         and n_micro > 1),
         },
         "prefill_ms": round(pre_ms, 3),
-        "prefill_timing": ("last micro-batch's prefill, overlapping the previous "
-                           "micro-batch's decode (Sampler.generate_many)"
+        "prefill_timing": (("last micro-batch's prefill in the kernel-timing pass "
+                            "(micro-batches run one after another)"
+                            if not args.no_kernel_timing else
+                            "last micro-batch's prefill, overlapping the previous "
+                            "micro-batch's decode (Sampler.generate_many)")
                            if args.decode and not args.no_pipeline and n_micro > 1
-                           and args.no_kernel_timing
-                           else "last micro-batch's prefill" + (
-                               " in the kernel-timing pass (micro-batches run one "
-                               "after another)" if not args.no_kernel_timing else "")),
+                           else "last micro-batch's prefill (headline pass)"),
         "prefill_tokens_per_s": round(prefill_tps, 1),
         "roofline": roofline_entry(ksum, dom, "mfma", args.config) if dom else None,
         "roofline_scan": roofline_entry(ksum, scan_key, "hbm", args.config)
