@@ -374,27 +374,19 @@ int main() {
     snprintf(nm, sizeof nm, "read 39.3 MB, %d blocks x 256", blocks);
     run_read(L, nm, 2560LL * 7680 * 2, blocks);
   }
+  printf("== down projection N=2560 K=7680 (39.3 MB): wider column tiles\n");
+  run_shipped<10>(L, "shipped stream<32,10,2> S3 combine (240 wg)", 2560, 7680, 3);
+  run_split<8, 5, 4, 1>(L, 2560, 7680, 6);
+  run_split<8, 4, 4, 1>(L, 2560, 7680, 8);
+  run_split<8, 8, 4, 1>(L, 2560, 7680, 4);
+  run_split<8, 10, 3, 1>(L, 2560, 7680, 3);
+  run_shipped<10>(L, "shipped stream<32,10,2> S3 combine (240 wg)", 2560, 7680, 3);
   printf("== out projection N=2560 K=2560 (13.1 MB)\n");
   run_shipped<5>(L, "shipped stream<32,5,2> S2 combine (160 wg)", 2560, 2560, 2);
-  run_split<4, 3, 1, 4>(L, 2560, 2560, 8);
-  run_split<4, 5, 1, 4>(L, 2560, 2560, 4);
-  run_split<4, 3, 2, 4>(L, 2560, 2560, 8);
-  run_split<4, 5, 2, 2>(L, 2560, 2560, 4);
-  run_split<8, 2, 1, 2>(L, 2560, 2560, 8);
-  run_split<8, 3, 1, 2>(L, 2560, 2560, 4);
-  run_split<8, 3, 2, 2>(L, 2560, 2560, 4);
-  run_split<8, 5, 2, 1>(L, 2560, 2560, 2);
-  printf("== down projection N=2560 K=7680 (39.3 MB)\n");
-  run_shipped<10>(L, "shipped stream<32,10,2> S3 combine (240 wg)", 2560, 7680, 3);
-  run_split<4, 8, 1, 4>(L, 2560, 7680, 8);
-  run_split<4, 15, 1, 2>(L, 2560, 7680, 4);
-  run_split<4, 8, 2, 2>(L, 2560, 7680, 8);
-  run_split<8, 4, 1, 2>(L, 2560, 7680, 8);
-  run_split<8, 5, 1, 2>(L, 2560, 7680, 6);
-  run_split<8, 8, 1, 2>(L, 2560, 7680, 4);
-  run_split<8, 8, 2, 1>(L, 2560, 7680, 4);
-  run_split<8, 4, 2, 1>(L, 2560, 7680, 8);
-  run_split<8, 10, 2, 1>(L, 2560, 7680, 3);
+  run_split<8, 2, 4, 1>(L, 2560, 2560, 5);
+  run_split<8, 3, 2, 1>(L, 2560, 2560, 4);
+  run_pipe<16, 5, 1, 1, 5>(L, "pipe nw16 nrep1 ch1x5 unsplit (160 wg)", 2560, 2560);
+  run_shipped<5>(L, "shipped stream<32,5,2> S2 combine (160 wg)", 2560, 2560, 2);
   printf("done\n");
   return 0;
 }
