@@ -1547,6 +1547,76 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
   }
 }
 
+// Decode residual projection of one K split (17..32 packed rows,
+// fragment-packed W, K <= 16 waves x KSW x 32): the 13 MB output projection
+// (K = 2560).  One workgroup = 16 output columns over all of K, 16 waves
+// streaming their k-steps in chunks of CH with INF chunks of weight +
+// activation fragments in flight; the EpiResidRows epilogue straight from the
+// fixed-order LDS reduction (no split, no combine trip).  Cold-weight lab
+// (tools/gemv_lab2.hip): 6.45-6.52 us against 6.98-7.06 for the 2-split
+// stream kernel with its in-kernel combine; the 39 MB down projection stays on
+// the split engine (per-CU bound unsplit: 15 us against 11.3).
+template <int NW, int KSW, int CH, int INF>
+__global__ __launch_bounds__(NW * 64) void gemm_resid_pipe_kernel(
+    const u16* __restrict__ A, const u16* __restrict__ W, int M, int K, EpiResidRows epi) {
+  constexpr int MR = 2, NC = KSW / CH;
+  static_assert(KSW % CH == 0 && INF <= NC && NW * 64 >= 32 * 16, "chunking / epilogue");
+  __shared__ float red[NW][32 * 16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const u16* zpage = reinterpret_cast<const u16*>(kZeroPage + lane);
+  const int ks32 = K >> 5;
+  const int col0 = blockIdx.x * 16;
+  // epilogue operands first: thread t < 512 owns (row t / 16, column t % 16)
+  const int pm = min((int)(threadIdx.x >> 4) & 31, M - 1);
+  const EpiResidRows::Pref pf = epi.prefetch(pm, col0 + (threadIdx.x & 15));
+  uint4 wb[INF][CH], xa[INF][CH][MR];
+  auto issue = [&](int c, int slot) {
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int k = (wave + NW * (c * CH + u)) * 32;
+      const bool ok = k < K;
+      wb[slot][u] = ld16_nt(ok ? W + (((int64_t)blockIdx.x * ks32 + (k >> 5)) * 64 + lane) * 8
+                               : zpage);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        xa[slot][u][i] = ld16(ok ? A + ((((int64_t)(k >> 5) * MR + i) * 64 + lane) << 3) : zpage);
+    }
+  };
+  f32x4 acc[MR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < INF; ++c) issue(c, c);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int slot = c % INF;
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8, xa[slot][u][i]), __builtin_bit_cast(bf16x8, wb[slot][u]),
+            acc[i], 0, 0, 0);
+    if (c + INF < NC) issue(c + INF, slot);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][(i * 16 + rsub + r) * 16 + csub] = acc[i][r];
+  __syncthreads();
+  const int o = threadIdx.x;
+  if (o >= 32 * 16) return;
+  const int m = o >> 4;
+  if (m >= M) return;
+  float v = 0.f;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) v += red[w][o];
+  epi.apply_pf(m, col0 + (o & 15), v, 0, pf);
+}
+
 // Decode gated up-projection (17..32 packed rows, fragment-packed W, one K
 // split): TWO gate / up pairs -- 64 packed columns, 32 features -- per
 // workgroup, so F = 7680 takes 240 workgroups, one round on the CUs (the
@@ -2720,6 +2790,14 @@ int cadence_gemm_linear_residual_rows(const void* A, int64_t lda, const void* W,
                 static_cast<const u16*>(resid), ld_resid, 0, RowMap{M, 0, 0}, 0.0f};
   epi.rows = static_cast<u16*>(out_rows);
   epi.mt = (int)((M + 15) / 16);
+  if (K == 2560 && M > 16 && lda == 0 && ldw == 0 && N % 16 == 0) {
+    // the output projection: unsplit, 16 waves per 16 columns
+    hipLaunchKernelGGL((gemm_resid_pipe_kernel<16, 5, 1, 5>), dim3((unsigned)(N / 16)),
+                       dim3(1024), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const u16*>(A), static_cast<const u16*>(W), (int)M,
+                       (int)K, epi);
+    return (int)hipGetLastError();
+  }
   launch_stream(static_cast<const u16*>(A), lda, static_cast<const u16*>(W), ldw, M, N,
                 K, 1, 0, 0, epi, ksw, ss, static_cast<float*>(workspace),
                 ldw == 0 ? 1 : 0, static_cast<hipStream_t>(stream), counters);

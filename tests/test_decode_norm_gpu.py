@@ -55,7 +55,12 @@ def test_residual_rows_match_two_kernel_path(dev, m, k):
   out1, n1 = ops.linear_rmsnorm(a, w, bias, resid, norm)
   out2, r2 = ops.linear_rmsnorm(a, w, bias, resid, norm, lazy=True)
   assert isinstance(r2, ops.PackedRows) and r2.norm is norm
-  assert torch.equal(out1, out2)
+  if k == 2560 and m > 16:
+    # the output projection's unsplit kernel (gemm_resid_pipe_kernel): one
+    # fp32 chain over all of K instead of the split-order sums
+    _close(out2, out1, frac=0.99)
+  else:
+    assert torch.equal(out1, out2)
   assert torch.equal(r2.unpack(), out2)
   _close(r2.normalised().unpack(), n1.unpack(), frac=0.999)
   # repeated launches reuse the (self-resetting) arrival counters
