@@ -388,6 +388,17 @@ struct EpiRowPref<E, std::void_t<decltype(E::kRowPref)>> {
   static constexpr bool value = E::kRowPref;
 };
 
+// Paired staged epilogues that combine gate and up in registers (kRegPair):
+// a lane's accumulator tiles j and j + 2 hold the gate and up columns of the
+// same features, so the output is computed before staging and only outputs
+// (half the values, no finish math) go through LDS.
+template <class E, class = void>
+struct EpiRegPair { static constexpr bool value = false; };
+template <class E>
+struct EpiRegPair<E, std::void_t<decltype(E::kRegPair)>> {
+  static constexpr bool value = E::kRegPair;
+};
+
 template <class E> struct EpiNormIn { static constexpr bool value = false; };
 
 struct EpiGatedGelu {
@@ -427,6 +438,18 @@ struct EpiGatedGelu {
 #pragma unroll
     for (int i = 0; i < 8; ++i) gv[i] = bmul(rbf(gelu_tanh(gv[i])), uv[i]);
     st16(out + xoff((int)m, f, ldo, mt), pack8(gv));
+  }
+  // big engine: gate x up of two rows in registers (big_epilogue kRegPair),
+  // the rounding points of stage() then finish8p(); packed bf16 pair out
+  static constexpr bool kRegPair = true;
+  CADENCE_DEV uint32_t out2(f32x2 g, f32x2 u, float bg, float bu) const {
+    const f32x2 gs = badd2(rbf2(g), f32x2{bg, bg});
+    const f32x2 us = badd2(rbf2(u), f32x2{bu, bu});
+    const f32x2 gl = rbf2(f32x2{gelu_tanh(gs.x), gelu_tanh(gs.y)});
+    return pk2bf(f32x2{mul_rn(gl.x, us.x), mul_rn(gl.y, us.y)});
+  }
+  CADENCE_DEV void store8(int64_t m, int f, uint4 v) const {
+    st16(out + xoff((int)m, f, ldo, mt), v);
   }
 };
 
@@ -737,7 +760,47 @@ CADENCE_DEV void big_epilogue(const Epi& epi, f32x4 (&acc)[MR][4], u16* st, int 
                               int nbase, int lane, int M, int N, int g) {
   constexpr int NR = 4;
   const int rsub = (lane >> 4) * 4, csub = lane & 15;
-  if constexpr (Epi::kStaged) {
+  if constexpr (Epi::kStaged && EpiRegPair<Epi>::value) {
+    // Gate x up in registers: output features obase + 16 h + csub, h = 0, 1
+    // (gate tiles 0 / 1, up tiles 2 / 3), rows taken in pairs (r, r + 1) so
+    // every rounding point rounds two values with one v_cvt_pk_bf16_f32; the
+    // bf16 outputs go to [16 MR rows][32 features] of the wave's LDS (16-B
+    // chunk XOR (row / 4) & 3: the 4 row groups of a write land on distinct
+    // banks), then 16-B row segments out.  Same operations and rounding
+    // points as stage() + finish8p(): bit-identical.
+    const int obase = nbase / 2;
+    float bgv[2], buv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bgv[h] = epi.bias_at(false, obase + h * 16 + csub, g);
+      buv[h] = epi.bias_at(true, obase + h * 16 + csub, g);
+    }
+    auto oidx = [](int r, int c) { return r * 32 + ((((c >> 3) ^ (r >> 2)) & 3) << 3) + (c & 7); };
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const uint32_t w = epi.out2(f32x2{acc[i][h][r], acc[i][h][r + 1]},
+                                      f32x2{acc[i][2 + h][r], acc[i][2 + h][r + 1]}, bgv[h],
+                                      buv[h]);
+          const int row = i * 16 + rsub + r, c = h * 16 + csub;
+          st[oidx(row, c)] = (u16)w;
+          st[oidx(row + 1, c)] = (u16)(w >> 16);
+        }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    // 4 chunks of 8 features per row, 16 rows per pass
+    const int ch = lane & 3;
+#pragma unroll
+    for (int it = 0; it < MR; ++it) {
+      const int lr = it * 16 + (lane >> 2);
+      const int row = mbase + lr;
+      const uint4 v = *reinterpret_cast<const uint4*>(&st[oidx(lr, ch * 8)]);
+      if (row < M) epi.store8(row, obase + ch * 8, v);
+    }
+  } else if constexpr (Epi::kStaged) {
     // Stage the wave's first-rounding-point bf16 values in its own 16 KiB of
     // the (now idle) operand LDS, [128 rows][64 cols] with a 16-B chunk XOR
     // swizzle (paired: cols 0..31 gate half, 32..63 up half of the same 32
