@@ -145,6 +145,35 @@ struct EpiLinearA : EpiLinear {
   }
 };
 
+// act 0 with a residual (the Griffin output / down projections): the
+// staged path loads the residual rows of every finish iteration before it
+// stages the accumulators (kResidPref), so the finish loop waits on one
+// memory trip instead of one per unrolled pair of iterations.  Same sums and
+// roundings as EpiLinearA<0> with `resid` set.
+template <>
+struct EpiLinearA<4> : EpiLinear {
+  static constexpr bool kResidPref = true;
+  CADENCE_DEV uint4 resid_at(int64_t m, int n) const { return ld16(resid + map(m) * ldr + n); }
+  CADENCE_DEV void finish8_r(int64_t m, int n, uint4 v, uint4 r) const {
+    float a[8], b[8];
+    unpack8(v, a);
+    unpack8(r, b);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = badd(a[i], b[i]);
+    st16(out + map(m) * ldo + n, pack8(a));
+  }
+  CADENCE_DEV void finish8(int64_t m, int n, uint4 v, int) const {
+    finish8_r(m, n, v, resid_at(m, n));
+  }
+};
+
+template <class E, class = void>
+struct EpiResidPref { static constexpr bool value = false; };
+template <class E>
+struct EpiResidPref<E, std::void_t<decltype(E::kResidPref)>> {
+  static constexpr bool value = E::kResidPref;
+};
+
 // Decode yx projection fused with the Conv1D decode step of the x branch
 // (stream engine only, M <= 32 rows = sequences): columns >= conv_lo are the
 // x branch; their rounded linear output x_t enters the depthwise causal
@@ -808,9 +837,21 @@ CADENCE_DEV void big_epilogue(const Epi& epi, f32x4 (&acc)[MR][4], u16* st, int 
     // lane and writes 16-B row segments.
     constexpr int OC = Epi::kPaired ? 32 : 64;     // output columns per wave
     constexpr int CPRW = OC / 8;                   // 16-B output chunks per row
+    constexpr int RPI = 64 / CPRW;                 // rows per finish iteration
     auto sidx = [&](int r, int c) {
       return r * 64 + (((c >> 3) ^ (r & 7)) << 3) + (c & 7);
     };
+    // kResidPref: every finish iteration's residual row segment is in flight
+    // while the accumulators are staged (rows / columns clamped in bounds)
+    constexpr bool kRP = EpiResidPref<Epi>::value;
+    constexpr int RIT = kRP ? MR * 16 / RPI : 1;
+    uint4 rpf[RIT];
+    if constexpr (kRP) {
+      const int col = min(nbase + (lane % CPRW) * 8, N - 8);
+#pragma unroll
+      for (int it = 0; it < RIT; ++it)
+        rpf[it] = epi.resid_at(min(mbase + it * RPI + lane / CPRW, M - 1), col);
+    }
     float bcol[NR];
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
@@ -837,9 +878,19 @@ CADENCE_DEV void big_epilogue(const Epi& epi, f32x4 (&acc)[MR][4], u16* st, int 
               (u16)(__float_as_uint(epi.stage(acc[i][j][r], bcol[j])) >> 16);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    constexpr int RPI = 64 / CPRW;                 // rows per iteration
     const int obase = Epi::kPaired ? nbase / 2 : nbase;
     const int ch = lane % CPRW;
+    if constexpr (kRP) {
+      const int col = obase + ch * 8;
+#pragma unroll
+      for (int it = 0; it < RIT; ++it) {
+        const int lr = it * RPI + lane / CPRW;
+        const int row = mbase + lr;
+        const uint4 v = *reinterpret_cast<const uint4*>(&st[lr * 64 + ((ch ^ (lr & 7)) << 3)]);
+        if (row < M && col < N) epi.finish8_r(row, col, v, rpf[it]);
+      }
+      return;
+    }
     if constexpr (EpiRowPref<Epi>::value) {
       constexpr int IT = MR * 16 / RPI;
       const int col = obase + ch * 8;
@@ -2371,9 +2422,10 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
 }
 
 // lab A/B switch of the prefill engines, a bit mask: bit 0 = the 4-wave
-// gemm_w4_kernel on its plans, bit 1 = rglru_gates_stream_kernel (0 = the
-// 8-wave block engine for everything)
-int g_engine = 3;
+// gemm_w4_kernel on its plans, bit 1 = rglru_gates_stream_kernel, bit 2 =
+// the residual-prefetching linear epilogue EpiLinearA<4> (0 = the 8-wave
+// block engine with the plain epilogues for everything)
+int g_engine = 7;
 
 // The 4-wave engine runs the wide long-K GEMMs (the gated MLP up-projection,
 // N = 2F = 15360, K = 2560) on 224 / 256-row tile plans.  Measured A/B in
@@ -2548,7 +2600,10 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
                           0, st, A, lda, W, ldw, (int)M, (int)N, (int)K, a_goff,        \
                           w_goff, EpiLinearA<ACT_>{epi})
       switch (epi.act) {
-        case 0: CADENCE_BIG_ACT(0); break;
+        case 0:
+          if (epi.resid && (g_engine & 4)) CADENCE_BIG_ACT(4);
+          else CADENCE_BIG_ACT(0);
+          break;
         case 1: CADENCE_BIG_ACT(1); break;
         case 2: CADENCE_BIG_ACT(2); break;
         case 3: CADENCE_BIG_ACT(3); break;

@@ -92,11 +92,12 @@ int cadence_gemm_big_splits(int64_t M, int64_t N, int64_t K, int64_t groups);
  * decode engines).  Host-side plan query. */
 int cadence_gemm_engine(int64_t M, int64_t N, int64_t K, int64_t groups);
 
-/* Lab A/B switch of the prefill engines, a bit mask (default 3): bit 0 =
+/* Lab A/B switch of the prefill engines, a bit mask (default 7): bit 0 =
  * the 4-wave gemm_w4_kernel for K >= 2048 on 224 / 256-row tile plans (else
  * the 8-wave gemm_big_kernel), bit 1 = prefill RG-LRU gates of 64 / 128 /
- * 256-wide blocks on rglru_gates_stream_kernel; 0 = the 8-wave block engine
- * for everything.  A negative value only queries.  Returns the previous
+ * 256-wide blocks on rglru_gates_stream_kernel, bit 2 = the linear GEMM with
+ * a residual loads its residual rows ahead of the staged epilogue (same
+ * bits); 0 = the 8-wave block engine with the plain epilogues for everything.  A negative value only queries.  Returns the previous
  * value.  Host state only. */
 int cadence_gemm_set_engine(int engine);
 

@@ -50,7 +50,7 @@ def ksweep(dev, lib):
       res[(K, eng)] = t
       print(f"ksweep K={K:5d} engine {eng}: {t:8.1f} us  {2 * M * N * K / t / 1e6:7.1f} TF/s",
             flush=True)
-  lib.cadence_gemm_set_engine(3)
+  lib.cadence_gemm_set_engine(7)
   for eng in (0, 1):
     ks = sorted({k for k, e in res if e == eng})
     xs = torch.tensor(ks, dtype=torch.float64)
@@ -102,7 +102,7 @@ def main():
       for eng in (0, 1):
         lib.cadence_gemm_set_engine(eng)
         times.setdefault((name, eng), []).append(timeit(run))
-  lib.cadence_gemm_set_engine(3)
+  lib.cadence_gemm_set_engine(7)
   for name, flops, run, grab in cases:
     t0, t1 = (sorted(times[(name, e)])[len(times[(name, e)]) // 2] for e in (0, 1))
     print(f"{name:34s} 8-wave {t0:8.1f} us {flops / t0 / 1e6:7.1f} TF/s | plan   "
