@@ -106,6 +106,12 @@ struct EpiLinear {
     if (bias) v = add_rn(v, b);
     return rbf(v);
   }
+  // stage() of two rows of one column, both bf16 in one word (kStage2)
+  static constexpr bool kStage2 = true;
+  CADENCE_DEV uint32_t stage2(f32x2 v, float b) const {
+    if (bias) v = f32x2{add_rn(v.x, b), add_rn(v.y, b)};
+    return pk2bf(v);
+  }
   template <class Act>
   CADENCE_DEV void finish8_with(int64_t m, int n, uint4 v, Act&& f) const {
     const int64_t orow = map(m);
@@ -165,6 +171,15 @@ struct EpiLinearA<4> : EpiLinear {
   CADENCE_DEV void finish8(int64_t m, int n, uint4 v, int) const {
     finish8_r(m, n, v, resid_at(m, n));
   }
+};
+
+// Staged epilogues whose first rounding point takes two rows at once
+// (stage2: one v_cvt_pk_bf16_f32 for both)
+template <class E, class = void>
+struct EpiStage2 { static constexpr bool value = false; };
+template <class E>
+struct EpiStage2<E, std::void_t<decltype(E::kStage2)>> {
+  static constexpr bool value = E::kStage2;
 };
 
 template <class E, class = void>
@@ -334,6 +349,8 @@ struct EpiRopeQKVBig {
   struct RowPref { uint2 sn, cs; };
   CADENCE_DEV float bias_at(bool, int, int) const { return 0.0f; }
   CADENCE_DEV float stage(float x, float) const { return rbf(x); }
+  static constexpr bool kStage2 = true;
+  CADENCE_DEV uint32_t stage2(f32x2 v, float) const { return pk2bf(v); }
   CADENCE_DEV int row_pos(int64_t m) const { return pos[m]; }
   // the table entries of columns n..n+7's four rotation pairs (rotated
   // columns inside the table only; the others read entry 0, unused)
@@ -868,14 +885,27 @@ CADENCE_DEV void big_epilogue(const Epi& epi, f32x4 (&acc)[MR][4], u16* st, int 
     for (int j = 0; j < NR; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) soff[j][r] = sidx(rsub + r, j * 16 + csub);
+    if constexpr (!Epi::kPaired && EpiStage2<Epi>::value) {
 #pragma unroll
-    for (int i = 0; i < MR; ++i)
+      for (int i = 0; i < MR; ++i)
 #pragma unroll
-      for (int j = 0; j < NR; ++j)
+        for (int j = 0; j < NR; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          st[i * 16 * 64 + soff[j][r]] =
-              (u16)(__float_as_uint(epi.stage(acc[i][j][r], bcol[j])) >> 16);
+          for (int r = 0; r < 4; r += 2) {
+            const uint32_t w = epi.stage2(f32x2{acc[i][j][r], acc[i][j][r + 1]}, bcol[j]);
+            st[i * 16 * 64 + soff[j][r]] = (u16)w;
+            st[i * 16 * 64 + soff[j][r + 1]] = (u16)(w >> 16);
+          }
+    } else {
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            st[i * 16 * 64 + soff[j][r]] =
+                (u16)(__float_as_uint(epi.stage(acc[i][j][r], bcol[j])) >> 16);
+    }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     const int obase = Epi::kPaired ? nbase / 2 : nbase;
