@@ -118,6 +118,39 @@ CADENCE_DEV float gelu_tanh(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + hw_exp(-2.0f * z));
 }
 
+// gelu_erf / gelu_tanh of two values: the same IEEE operations in the same
+// order (bit-identical per element), with the multiplies, adds and fmas on
+// packed fp32 (v_pk_mul / v_pk_add / v_pk_fma_f32, two values per
+// instruction); only the transcendentals run per element.
+CADENCE_DEV f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+CADENCE_DEV f32x2 splat2(float v) { return f32x2{v, v}; }
+CADENCE_DEV f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 z = __builtin_elementwise_abs(x) * splat2(0.70710678118654752440f);
+  const f32x2 d = splat2(1.0f) + splat2(0.5f) * z;
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = splat2(0.17087277f);
+  p = fma2(p, t, splat2(-0.82215223f));
+  p = fma2(p, t, splat2(1.48851587f));
+  p = fma2(p, t, splat2(-1.13520398f));
+  p = fma2(p, t, splat2(0.27886807f));
+  p = fma2(p, t, splat2(-0.18628806f));
+  p = fma2(p, t, splat2(0.09678418f));
+  p = fma2(p, t, splat2(0.37409196f));
+  p = fma2(p, t, splat2(1.00002368f));
+  p = fma2(p, t, splat2(-1.26551223f));
+  const f32x2 ea = (p - z * z) * splat2(1.4426950408889634f);
+  const f32x2 q = t * f32x2{__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+  const f32x2 two_q = splat2(2.0f) - q;
+  const f32x2 s = f32x2{x.x >= 0.0f ? two_q.x : q.x, x.y >= 0.0f ? two_q.y : q.y};
+  return splat2(0.5f) * x * s;
+}
+CADENCE_DEV f32x2 gelu_tanh2(f32x2 x) {
+  const f32x2 z = splat2(0.7978845608028654f) * (x + splat2(0.044715f) * x * x * x);
+  const f32x2 ea = (splat2(-2.0f) * z) * splat2(1.4426950408889634f);
+  const f32x2 d = splat2(1.0f) + f32x2{__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+  return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
 // 16-byte vector of 8 bf16 (raw) for global/LDS traffic.
 struct alignas(16) u16x8 {
   u16 v[8];

@@ -142,6 +142,19 @@ struct EpiLinearA : EpiLinear {
         return;
       }
     }
+    if constexpr (ACT == 1 || ACT == 3) {
+      if (!resid) {             // GELU of 4 packed pairs (gelu_erf2 / gelu_tanh2)
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f32x2 a{__uint_as_float(w[k] << 16), __uint_as_float(w[k] & 0xffff0000u)};
+          o[k] = pk2bf(ACT == 1 ? gelu_erf2(a) : gelu_tanh2(a));
+        }
+        st16(out + map(m) * ldo + n, make_uint4(o[0], o[1], o[2], o[3]));
+        return;
+      }
+    }
     finish8_with(m, n, v, [&](float r) {
       if constexpr (ACT == 1) r = rbf(gelu_erf(r));
       if constexpr (ACT == 2) r = softcap(r, cap);
@@ -491,7 +504,7 @@ struct EpiGatedGelu {
   CADENCE_DEV uint32_t out2(f32x2 g, f32x2 u, float bg, float bu) const {
     const f32x2 gs = badd2(rbf2(g), f32x2{bg, bg});
     const f32x2 us = badd2(rbf2(u), f32x2{bu, bu});
-    const f32x2 gl = rbf2(f32x2{gelu_tanh(gs.x), gelu_tanh(gs.y)});
+    const f32x2 gl = rbf2(gelu_tanh2(gs));
     return pk2bf(f32x2{mul_rn(gl.x, us.x), mul_rn(gl.y, us.y)});
   }
   CADENCE_DEV void store8(int64_t m, int f, uint4 v) const {
