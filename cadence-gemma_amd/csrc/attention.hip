@@ -45,8 +45,16 @@ constexpr int MODE_VIT = 1;
 constexpr int KT = 32;  // keys per tile
 constexpr int kDecodeSplitsMax = 32;  // window ranges of the decode attention
 // ranges per sequence: enough workgroups to cover the CUs at any batch
+// (lab knobs, read once: CADENCE_DEC_F = workgroups per batch to spread the
+// ranges over, CADENCE_DEC_CMIN = fewest keys per range)
+inline int dec_env(const char* n, int dflt) {
+  const char* v = getenv(n);
+  return v && *v ? atoi(v) : dflt;
+}
+inline int decode_f() { static const int f = dec_env("CADENCE_DEC_F", 256); return f; }
+inline int decode_cmin() { static const int c = dec_env("CADENCE_DEC_CMIN", 64); return c; }
 inline int decode_splits(int64_t B) {
-  const int64_t ns = 256 / (B > 0 ? B : 1);
+  const int64_t ns = decode_f() / (B > 0 ? B : 1);
   return (int)(ns < 1 ? 1 : ns > kDecodeSplitsMax ? kDecodeSplitsMax : ns);
 }
 
@@ -291,12 +299,17 @@ struct DecodeArgs {
   float scale;
   float* parts;           // [B, NS, 32 + 16 * hd] fp32 split partials (NS > 1)
   int32_t* sems;          // [B] zeroed arrival counters (NS > 1)
+  int cmin;               // fewest keys per range (a multiple of 16)
 };
 
 // Split over the window (gridDim.y = NS): the B x NS workgroups cover the
 // sequence's non-empty keys -- ring slots [0, slot_hi) then the new key,
 // nk = slot_hi + 1 in all -- in NS contiguous ranges of C = ceil(nk / NS)
-// keys rounded up to 16 (ranges past nk exit at once).  A range is streamed
+// keys rounded up to 16, at least cmin = 64 (ranges past nk exit at once:
+// every range costs the combine a partial, and the combine's trip is the
+// dearest link of the chain -- tools/decode_attn_lab.sh, profiles/r03ad_*:
+// B = 32 at 320 keys 15.6 -> 14.6 us, at 64 keys 13.5 -> 11.9; more, shorter
+// ranges per sequence were slower at every context).  A range is streamed
 // in tiles of 64 keys: every K and V byte of the tile is loaded up front into
 // registers (the next tile's loads go out as soon as this one is in LDS), K
 // is stored with the row swizzle of the QK^T fragment reads, V row-major with
@@ -344,7 +357,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
   // slots with a non-negative position: all of them once the ring wrapped
   const int slot_hi = nt >= a.W ? a.W : nt;
   const int nk = slot_hi + 1;                   // + the new key
-  const int C = (((nk + NS - 1) / NS) + 15) & ~15;
+  const int C = max(a.cmin, (((nk + NS - 1) / NS) + 15) & ~15);
   const int nsp = (nk + C - 1) / C;             // active ranges
   if (split >= nsp) return;
   const int kb = split * C, ke = min(nk, kb + C);
@@ -854,7 +867,7 @@ int cadence_local_attention_decode(const void* q, const void* k_new,
                num_tokens, static_cast<u16*>(out), ld_out, (int)((B + 15) / 16),
                (int)H, (int)hd,
                (int)window, 1.0f / sqrtf((float)hd),
-               static_cast<float*>(workspace), sems};
+               static_cast<float*>(workspace), sems, decode_cmin()};
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)B, split ? decode_splits(B) : 1);
   if (hd == 256)
