@@ -45,16 +45,10 @@ constexpr int MODE_VIT = 1;
 constexpr int KT = 32;  // keys per tile
 constexpr int kDecodeSplitsMax = 32;  // window ranges of the decode attention
 // ranges per sequence: enough workgroups to cover the CUs at any batch
-// (lab knobs, read once: CADENCE_DEC_F = workgroups per batch to spread the
-// ranges over, CADENCE_DEC_CMIN = fewest keys per range)
-inline int dec_env(const char* n, int dflt) {
-  const char* v = getenv(n);
-  return v && *v ? atoi(v) : dflt;
-}
-inline int decode_f() { static const int f = dec_env("CADENCE_DEC_F", 256); return f; }
-inline int decode_cmin() { static const int c = dec_env("CADENCE_DEC_CMIN", 64); return c; }
+// fewest keys per range (a multiple of 16; see decode_attn_kernel's plan)
+constexpr int kDecodeMinRange = 64;
 inline int decode_splits(int64_t B) {
-  const int64_t ns = decode_f() / (B > 0 ? B : 1);
+  const int64_t ns = 256 / (B > 0 ? B : 1);
   return (int)(ns < 1 ? 1 : ns > kDecodeSplitsMax ? kDecodeSplitsMax : ns);
 }
 
@@ -867,7 +861,7 @@ int cadence_local_attention_decode(const void* q, const void* k_new,
                num_tokens, static_cast<u16*>(out), ld_out, (int)((B + 15) / 16),
                (int)H, (int)hd,
                (int)window, 1.0f / sqrtf((float)hd),
-               static_cast<float*>(workspace), sems, decode_cmin()};
+               static_cast<float*>(workspace), sems, kDecodeMinRange};
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)B, split ? decode_splits(B) : 1);
   if (hd == 256)

@@ -1,6 +1,9 @@
 #!/bin/bash
 # Decode attention split plan sweep (CADENCE_DEC_F workgroups per batch,
 # CADENCE_DEC_CMIN fewest keys per range) on tools/decode_attn_micro.py.
+# The two knobs were environment variables of the lab build of commit
+# b29c322 only (the shipped library reads no environment: F = 256,
+# kDecodeMinRange = 64 are compile-time constants of attention.hip).
 # usage: tools/decode_attn_lab.sh TAG
 set -o pipefail
 tag=${1:?tag}
