@@ -153,6 +153,118 @@ __global__ __launch_bounds__(256) void conv1d_prefill_tw_kernel(
   }
 }
 
+// conv1d_prefill_tw_kernel's arithmetic for TS consecutive time steps of one
+// 8-channel chunk per thread: the TS + TW - 1 input rows, the TW weight rows
+// and the bias are loaded and unpacked once (instead of TW row loads and
+// unpacks per output), and the products / sums run on channel pairs
+// (v_pk_mul / v_pk_add_f32 + one v_cvt_pk_bf16_f32 per rounding point of two
+// channels: bmul2 / badd2).  Same terms in the same order (s = 0 .. TW-1,
+// then + bias) with the same bf16 roundings, and a masked tap still adds
+// bf16(0 * w) (signed zero included): bitwise equal to the one-step kernel.
+// Threads whose outputs all keep every tap (no document start in reach: the
+// common case) skip the mask selects.
+template <int TW, int TS>
+__global__ __launch_bounds__(256) void conv1d_prefill_ts_kernel(
+    const u16* __restrict__ x, int64_t ldx, const u16* __restrict__ w,
+    const u16* __restrict__ bias, const int32_t* __restrict__ pos,
+    u16* __restrict__ out, int64_t ldo, u16* __restrict__ cache_out, int B,
+    int L, int E, int compat) {
+  constexpr int NR = TS + TW - 1;            // input rows t0 - (TW-1) .. t0 + TS - 1
+  const int ch8 = E / 8;
+  const int ng = (L + TS - 1) / TS;
+  const int64_t total = (int64_t)B * ng * ch8;
+  for (int64_t idx = blockIdx.x * 256 + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * 256) {
+    const int c = idx % ch8;
+    const int64_t bg = idx / ch8;
+    const int t0 = (int)(bg % ng) * TS, b = (int)(bg / ng);
+    const int e0 = c * 8;
+    const int64_t row0 = (int64_t)b * L;
+    // row r holds time t0 - (TW-1) + r, clamped into [0, L - 1]
+    uint4 xr[NR], wr[TW];
+    bool nz[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int tt = min(max(t0 - (TW - 1) + r, 0), L - 1);
+      xr[r] = ld16(x + (row0 + tt) * ldx + e0);
+    }
+#pragma unroll
+    for (int s = 0; s < TW; ++s) wr[s] = ld16(w + (int64_t)(TW - 1 - s) * E + e0);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int tt = min(max(t0 - (TW - 1) + r, 0), L - 1);
+      nz[r] = pos[row0 + tt] != 0;
+    }
+    const uint4 br = ld16(bias + e0);
+    // keep(i, s): output t = t0 + i, tap s reads row i + TW-1 - s; its mask
+    // needs pos[t - s + k] != 0 for k = 1..look (rows i + TW-1 - s + k)
+    bool keep[TS][TW];
+    bool all = true;
+#pragma unroll
+    for (int i = 0; i < TS; ++i)
+#pragma unroll
+      for (int s = 0; s < TW; ++s) {
+        const int look = compat ? s - 2 : s;
+        bool k_ = t0 + i - s >= 0;
+#pragma unroll
+        for (int k = 1; k <= TW; ++k)
+          if (k <= look) k_ = k_ && nz[i + TW - 1 - s + k];
+        keep[i][s] = k_;
+        if (t0 + i < L && s < L) all = all && k_;
+      }
+    f32x2 xv[NR][4], wv[TW][4], bv[4];
+    auto unpack = [](uint4 q, f32x2 (&o)[4]) {
+      const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = f32x2{__uint_as_float(u[j] << 16), __uint_as_float(u[j] & 0xffff0000u)};
+    };
+#pragma unroll
+    for (int r = 0; r < NR; ++r) unpack(xr[r], xv[r]);
+#pragma unroll
+    for (int s = 0; s < TW; ++s) unpack(wr[s], wv[s]);
+    unpack(br, bv);
+    auto outputs = [&](auto masked) {
+#pragma unroll
+      for (int i = 0; i < TS; ++i) {
+        const int t = t0 + i;
+        f32x2 acc[4];
+#pragma unroll
+        for (int s = 0; s < TW; ++s) {
+          if (s >= L) break;   // taps past the sequence are skipped, not added as 0
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            f32x2 xs = xv[i + TW - 1 - s][j];
+            if constexpr (decltype(masked)::value)
+              xs = keep[i][s] ? xs : f32x2{0.0f, 0.0f};
+            const f32x2 term = bmul2(xs, wv[s][j]);
+            acc[j] = s == 0 ? term : badd2(acc[j], term);
+          }
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = pk2bf(f32x2{add_rn(acc[j].x, bv[j].x),
+                                                       add_rn(acc[j].y, bv[j].y)});
+        if (t < L) st16(out + (row0 + t) * ldo + e0, make_uint4(o[0], o[1], o[2], o[3]));
+      }
+    };
+    if (all) outputs(std::false_type{});
+    else outputs(std::true_type{});
+    if (cache_out) {
+#pragma unroll
+      for (int i = 0; i < TS; ++i) {
+        const int t = t0 + i;
+        if (t < L && t >= L - (TW - 1))
+          st16(cache_out + ((int64_t)b * (TW - 1) + (t - (L - (TW - 1)))) * E + e0,
+               xr[i + TW - 1]);
+      }
+      if (t0 == 0 && L < TW - 1)
+        for (int slot = 0; slot < TW - 1 - L; ++slot)
+          st16(cache_out + ((int64_t)b * (TW - 1) + slot) * E + e0, make_uint4(0, 0, 0, 0));
+    }
+  }
+}
+
 // Single-token decode: full = [state (TW-1 rows), x]; no document mask
 // (layers.py:478-483).  cache_out may alias cache_in (each thread reads its
 // 8 channels of every state row before writing them).
@@ -544,7 +656,15 @@ int cadence_conv1d(const void* x, int64_t ldx, const void* w, const void* b,
 #undef CADENCE_CONV_TW
     }
   } else {
-    if (temporal_width == 4)
+    if (temporal_width == 4 && L >= 4)
+      hipLaunchKernelGGL((conv1d_prefill_ts_kernel<4, 4>),
+                         dim3(grid_for(B * ((L + 3) / 4) * E / 8)),
+                         dim3(256), 0, st, static_cast<const u16*>(x), ldx,
+                         static_cast<const u16*>(w), static_cast<const u16*>(b),
+                         segment_pos, static_cast<u16*>(out), ldo,
+                         static_cast<u16*>(cache_out), (int)B, (int)L, (int)E,
+                         compat);
+    else if (temporal_width == 4)
       hipLaunchKernelGGL(conv1d_prefill_tw_kernel<4>, dim3(grid_for(B * L * E / 8)),
                          dim3(256), 0, st, static_cast<const u16*>(x), ldx,
                          static_cast<const u16*>(w), static_cast<const u16*>(b),

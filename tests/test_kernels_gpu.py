@@ -124,8 +124,12 @@ def test_rnn_scan_gated_matches_join(dev, t, e, strided, with_h0):
 # ---------------------------------------------------------------- conv1d
 
 @pytest.mark.parametrize("compat", [True, False])
-@pytest.mark.parametrize("b,t,e", [(2, 40, 128), (1, 2, 64), (3, 97, 2560)])
+@pytest.mark.parametrize("b,t,e", [(2, 40, 128), (1, 2, 64), (3, 97, 2560),
+                                   (2, 4, 64), (2, 5, 64), (3, 7, 128), (4, 319, 2560)])
 def test_conv1d_prefill_bitexact(dev, compat, b, t, e):
+  """Conv1D prefill vs the oracle, bitwise: L < 4 (one-step kernel), L >= 4
+  (four time steps per thread: ragged last groups, document starts inside
+  a group, the bench's 319-step rows)."""
   g = torch.Generator().manual_seed(2)
   x = rnd(b, t, e, gen=g)
   w = rnd(4, e, scale=0.5, gen=g)
