@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -86,6 +86,7 @@ _SIGS: dict[str, list] = {
     "cadence_local_attention_cached": [P, P, P, P, P, P, P, I64, I64, I64, I64,
                                        I64, P],
     "cadence_kv_ring_update": [P, P, P, P, P, I64, I64, I64, P],
+    "cadence_copy_batched": [P, I64, P],
     "cadence_decode_advance": [P, P, I64, P, P, P, P, I32, I32, I32, I64, P],
 }
 _RESTYPE = {
@@ -95,6 +96,12 @@ _RESTYPE = {
     "cadence_logits_scratch_bytes": I64,
     "cadence_rnn_scan_workspace_bytes": I64,
 }
+
+
+class CopyDesc(ctypes.Structure):
+  """CadenceCopyDesc (cadence_kernels.h): one row-strided copy region."""
+  _fields_ = [("src", P), ("dst", P), ("rows", I64), ("row_bytes", I64),
+              ("src_stride", I64), ("dst_stride", I64)]
 
 
 class KernelLibraryMissing(RuntimeError):

@@ -184,6 +184,43 @@ def _counters(dev: torch.device, n: int):
   return buf
 
 
+def _copy_region(dst: torch.Tensor, src: torch.Tensor):
+  """(rows, row_bytes, src_stride, dst_stride) of a dst <- src copy whose
+  views are each [rows, contiguous rest] (a whole contiguous tensor is one
+  row), or None when the layout does not fit that form."""
+  if dst.shape != src.shape or dst.dtype != src.dtype or dst.device != src.device:
+    return None
+  es = dst.element_size()
+  if dst.is_contiguous() and src.is_contiguous():
+    return 1, dst.numel() * es, 0, 0
+  if dst.dim() < 2 or not (dst[0].is_contiguous() and src[0].is_contiguous()):
+    return None
+  return dst.shape[0], dst[0].numel() * es, src.stride(0) * es, dst.stride(0) * es
+
+
+def copy_batched_(pairs) -> None:
+  """dst.copy_(src) for every (dst, src) pair on the current stream, the
+  row-strided ones batched into cadence_copy_batched launches (one per 32
+  regions) instead of one copy kernel each; pairs that do not fit its
+  layout (or 4-byte granularity) fall back to Tensor.copy_."""
+  descs = []
+  dev = None
+  for dst, src in pairs:
+    reg = _copy_region(dst, src) if dst.is_cuda else None
+    if reg is None or reg[1] % 4 or reg[2] % 4 or reg[3] % 4 or \
+        dst.data_ptr() % 4 or src.data_ptr() % 4:
+      dst.copy_(src)
+      continue
+    if reg[0] * reg[1] == 0:
+      continue
+    dev = dst
+    descs.append(_lib.CopyDesc(src.data_ptr(), dst.data_ptr(), *reg))
+  if descs:
+    arr = (_lib.CopyDesc * len(descs))(*descs)
+    _lib.check(_lib.load().cadence_copy_batched(arr, len(descs), _s(dev)),
+               "copy_batched")
+
+
 def claim_counters(stream: torch.cuda.Stream, owner) -> None:
   """Ties the counter buffer of `stream` to `owner` (a captured decode graph,
   whose kernels hold its raw pointer): the owner keeps the buffer alive, and

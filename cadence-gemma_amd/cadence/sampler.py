@@ -445,15 +445,14 @@ class _DecodeGraph:
   def _copy_cache(dst_cache, src_cache, slots):
     """Copies block caches; of the attention ring buffers only the first
     `slots` slots (the ones written so far; decode attention never reads a
-    slot at or past num_tokens before the ring wraps), all when None."""
-    for name, src in src_cache.items():
-      dst = dst_cache[name]
-      ring = isinstance(src, AttentionBlockCache) and slots is not None
-      for d, s_ in zip(dst, src):
-        if ring and d.dim() == 4 and slots < d.shape[1]:
-          d[:, :slots].copy_(s_[:, :slots])
-        else:
-          d.copy_(s_)
+    slot at or past num_tokens before the ring wraps), all when None:
+    the (dst, src) pairs, for one ops.copy_batched_ with the other
+    hand-over copies."""
+    return [(d[:, :slots], s_[:, :slots])
+            if (isinstance(src, AttentionBlockCache) and slots is not None and
+                d.dim() == 4 and slots < d.shape[1]) else (d, s_)
+            for name, src in src_cache.items()
+            for d, s_ in zip(dst_cache[name], src)]
 
   def run(self, cache, cur, pos, buf, step, n_more, events=None, start=1,
           cache_len=None, done_in=None):
@@ -462,16 +461,16 @@ class _DecodeGraph:
     `cache_len`: tokens already in the attention caches (host-known), so
     only written ring slots move.  Returns the per-row done flags."""
     steps = buf.shape[1]
-    self._copy_cache(self.cache, cache, cache_len)
-    self.cur.copy_(cur)
-    self.pos.copy_(pos)
+    # the prefill state in: cache, token, position, buffer (no columns left
+    # from an earlier run), flags -- one batched copy launch
+    pairs = self._copy_cache(self.cache, cache, cache_len)
+    pairs += [(self.cur, cur), (self.pos, pos), (self.buf[:, :steps], buf)]
+    if self.done is not None and done_in is not None:
+      pairs.append((self.done, done_in))
+    ops.copy_batched_(pairs)
     self.step.fill_(start)
-    self.buf[:, :steps].copy_(buf)        # no columns left from an earlier run
-    if self.done is not None:
-      if done_in is not None:
-        self.done.copy_(done_in)
-      else:
-        self.done.zero_()
+    if self.done is not None and done_in is None:
+      self.done.zero_()
     watch = _DoneWatch(self.done)
     if events is not None:   # the replays alone (cache copies excluded)
       events["decode_start"] = torch.cuda.Event(enable_timing=True)
@@ -487,10 +486,9 @@ class _DecodeGraph:
         done += 1
     if events is not None:
       events["decode_end"].record()
-    buf[:, start:].copy_(self.buf[:, start:steps])
-    step.copy_(self.step)
-    pos.copy_(self.pos)
-    cur.copy_(self.cur)
-    self._copy_cache(cache, self.cache,
-                     None if cache_len is None else cache_len + done)
+    pairs = [(buf[:, start:], self.buf[:, start:steps]), (step, self.step),
+             (pos, self.pos), (cur, self.cur)]
+    pairs += self._copy_cache(cache, self.cache,
+                              None if cache_len is None else cache_len + done)
+    ops.copy_batched_(pairs)
     return _row_done(self.done, cur.shape[0], cur.device).clone()

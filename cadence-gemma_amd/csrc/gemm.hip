@@ -2722,7 +2722,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 13; }
+int cadence_abi_version(void) { return 14; }
 
 int cadence_gemm_set_engine(int engine) {
   const int prev = g_engine;

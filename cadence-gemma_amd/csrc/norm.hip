@@ -291,6 +291,33 @@ __global__ void decode_advance_kernel(const int32_t* __restrict__ next,
   }
 }
 
+// Batched row-strided device copies (the decode graph's cache hand-over):
+// blockIdx.y = descriptor, blocks grid-stride over its 16-B (or 4-B) units.
+constexpr int kCopyBatch = 32;
+struct CopyBatch {
+  CadenceCopyDesc d[kCopyBatch];
+};
+__global__ __launch_bounds__(256) void copy_batched_kernel(CopyBatch cb) {
+  const CadenceCopyDesc d = cb.d[blockIdx.y];
+  const bool wide = d.row_bytes % 16 == 0 && d.src_stride % 16 == 0 &&
+                    d.dst_stride % 16 == 0 && (uintptr_t)d.src % 16 == 0 &&
+                    (uintptr_t)d.dst % 16 == 0;
+  const int64_t unit = wide ? 16 : 4;
+  const int64_t per_row = d.row_bytes / unit, total = d.rows * per_row;
+  const char* src = static_cast<const char*>(d.src);
+  char* dst = static_cast<char*>(d.dst);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / per_row, c = (i % per_row) * unit;
+    if (wide)
+      *reinterpret_cast<uint4*>(dst + r * d.dst_stride + c) =
+          *reinterpret_cast<const uint4*>(src + r * d.src_stride + c);
+    else
+      *reinterpret_cast<uint32_t*>(dst + r * d.dst_stride + c) =
+          *reinterpret_cast<const uint32_t*>(src + r * d.src_stride + c);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -364,6 +391,38 @@ int cadence_embed(const int32_t* tokens, const void* E, void* out,
                      static_cast<const u16*>(E), static_cast<u16*>(out), ldo, M,
                      (int)D, V, scale, row_div, row_mul, row_off);
   return (int)hipGetLastError();
+}
+
+int cadence_copy_batched(const CadenceCopyDesc* desc, int64_t n, void* stream) {
+  if (n < 0 || (n > 0 && !desc)) return (int)hipErrorInvalidValue;
+  for (int64_t i = 0; i < n; ++i) {
+    const CadenceCopyDesc& d = desc[i];
+    if (d.rows < 0 || d.row_bytes < 0 || d.row_bytes % 4 || d.src_stride % 4 ||
+        d.dst_stride % 4 || (uintptr_t)d.src % 4 || (uintptr_t)d.dst % 4 ||
+        (d.rows > 1 && (d.src_stride < d.row_bytes || d.dst_stride < d.row_bytes)) ||
+        (d.rows * d.row_bytes > 0 && (!d.src || !d.dst)))
+      return (int)hipErrorInvalidValue;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  bool launched = false;
+  for (int64_t i0 = 0; i0 < n; i0 += kCopyBatch) {
+    CopyBatch cb{};
+    const int m = (int)(n - i0 < kCopyBatch ? n - i0 : kCopyBatch);
+    int64_t most = 0;
+    for (int j = 0; j < m; ++j) {
+      cb.d[j] = desc[i0 + j];
+      const int64_t units = cb.d[j].rows * (cb.d[j].row_bytes / 4);
+      most = units > most ? units : most;
+    }
+    if (most == 0) continue;
+    // ~4 (wide) units per thread for the largest region, at most 1024 blocks
+    int64_t g = (most / 4 + 1023) / 1024;
+    g = g < 1 ? 1 : g > 1024 ? 1024 : g;
+    hipLaunchKernelGGL(copy_batched_kernel, dim3((unsigned)g, (unsigned)m), dim3(256), 0,
+                       st, cb);
+    launched = true;
+  }
+  return launched ? (int)hipGetLastError() : 0;
 }
 
 int cadence_splice_positions(const int32_t* text_pos, int32_t* out,

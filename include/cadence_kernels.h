@@ -468,6 +468,20 @@ int cadence_local_attention_cached(const void* q, const void* k_new,
                                    int64_t B, int64_t T, int64_t H, int64_t hd,
                                    int64_t window, void* stream);
 
+/* Batched device-to-device copies in one launch per 32 descriptors: region
+ * i is desc[i].rows rows of desc[i].row_bytes bytes, consecutive rows
+ * src_stride / dst_stride bytes apart.  Sizes, strides and pointers are
+ * multiples of 4 bytes (16 for the wide path).  Regions must not overlap.
+ * Replaces the per-tensor copies of the decode graph's cache hand-over
+ * (the host side of recurrentgemma/torch/sampler.py:209-225 keeps the
+ * prefill cache and the step cache as separate tensors). */
+typedef struct CadenceCopyDesc {
+  const void* src;
+  void* dst;
+  int64_t rows, row_bytes, src_stride, dst_stride;
+} CadenceCopyDesc;
+int cadence_copy_batched(const CadenceCopyDesc* desc, int64_t n, void* stream);
+
 /* Single-token ring update (modules.py:206-215): slot num_tokens[b] % window
  * <- k_new[b] / v_new[b]; num_tokens[b] += 1. */
 int cadence_kv_ring_update(const void* k_new, const void* v_new, void* cache_k,

@@ -29,6 +29,19 @@ def test_library_loads_and_exports_every_declared_symbol():
   assert lib.cadence_abi_version() == _lib.ABI_VERSION
 
 
+def test_copy_batched_contract_without_gpu():
+  lib = _lib.load()
+  assert lib.cadence_copy_batched(None, 0, None) == 0          # nothing to do
+  bad = (_lib.CopyDesc * 1)(_lib.CopyDesc(16, 32, 1, 6, 0, 0))   # 6-byte rows
+  assert lib.cadence_copy_batched(bad, 1, None) != 0
+  bad = (_lib.CopyDesc * 1)(_lib.CopyDesc(18, 32, 1, 8, 0, 0))   # misaligned src
+  assert lib.cadence_copy_batched(bad, 1, None) != 0
+  bad = (_lib.CopyDesc * 1)(_lib.CopyDesc(16, 32, 2, 64, 32, 64))  # stride < row
+  assert lib.cadence_copy_batched(bad, 1, None) != 0
+  empty = (_lib.CopyDesc * 1)(_lib.CopyDesc(None, None, 0, 0, 0, 0))
+  assert lib.cadence_copy_batched(empty, 1, None) == 0
+
+
 def test_host_contract_checks_without_gpu():
   lib = _lib.load()
   # workspace query is host-only arithmetic

@@ -638,3 +638,38 @@ def test_segment_info(dev, b, l):
   want_start = torch.cummax(last, 1).values
   assert torch.equal(seg.cpu(), want_seg.to(torch.int32))
   assert torch.equal(start.cpu(), want_start.to(torch.int32))
+
+
+def test_copy_batched_matches_tensor_copies(dev):
+  """ops.copy_batched_ (cadence_copy_batched, one launch per 32 regions):
+  the decode graph's hand-over copies -- ring-buffer slot prefixes
+  [B, :slots], contiguous states, 4-byte int32 vectors, bf16 rows with a
+  column offset -- equal Tensor.copy_ bitwise, over more than one batch of
+  32 descriptors."""
+  g = torch.Generator().manual_seed(31)
+  pairs, want = [], []
+  for i in range(40):
+    b = 1 + i % 3
+    if i % 4 == 0:
+      src = rnd(b, 64, 1, 32, gen=g).to(dev)
+      dst = torch.zeros_like(src)
+      s = 1 + i % 50
+      pairs.append((dst[:, :s], src[:, :s]))
+      w = dst.clone(); w[:, :s] = src[:, :s]; want.append((dst, w))
+    elif i % 4 == 1:
+      src = torch.randn(b, 96, generator=g).to(dev)
+      dst = torch.zeros_like(src)
+      pairs.append((dst, src)); want.append((dst, src.clone()))
+    elif i % 4 == 2:
+      src = torch.randint(0, 1000, (b,), dtype=torch.int32, generator=g).to(dev)
+      dst = torch.zeros_like(src)
+      pairs.append((dst, src)); want.append((dst, src.clone()))
+    else:
+      src = torch.randint(0, 1000, (b, 10), dtype=torch.int32, generator=g).to(dev)
+      dst = torch.zeros(b, 12, dtype=torch.int32, device=dev)
+      pairs.append((dst[:, 3:], src[:, 1:10]))
+      w = dst.clone(); w[:, 3:] = src[:, 1:10]; want.append((dst, w))
+  ops.copy_batched_(pairs)
+  torch.cuda.synchronize()
+  for dst, w in want:
+    assert torch.equal(dst.cpu(), w.cpu())
