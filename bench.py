@@ -332,7 +332,7 @@ def main():
   rank, world, local = D.init_from_env()
   if world != args.gpus and rank == 0:
     print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-  dev = torch.device("cuda", local)
+  dev = torch.device("cuda", D.local_device_index(local))
   torch.cuda.set_device(dev)
   if args.gemm_engine is not None:
     from cadence import _lib

@@ -24,15 +24,28 @@ def env_world() -> tuple[int, int, int]:
           int(os.environ.get("LOCAL_RANK", 0)))
 
 
+def local_device_index(local: int) -> int:
+  """The GPU of local rank `local`: its own on a node with one GPU per rank
+  (the identity there); ranks past the visible GPUs wrap onto them, which
+  only a multi-rank rehearsal on a smaller box uses (with the gloo backend:
+  RCCL refuses two ranks on one GPU)."""
+  n = torch.cuda.device_count()
+  return local % n if n > 0 else local
+
+
 def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
+  """(rank, world, local rank); joins the process group when world > 1.
+  Backend: `backend`, else $CADENCE_DIST_BACKEND, else "nccl" (RCCL) on a
+  GPU host and "gloo" on CPU."""
   rank, world, local = env_world()
   if world > 1 and not dist.is_initialized():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
-      backend = "nccl" if torch.cuda.is_available() else "gloo"
+      backend = os.environ.get("CADENCE_DIST_BACKEND") or (
+          "nccl" if torch.cuda.is_available() else "gloo")
     kw = {}
     if backend == "nccl":
-      kw["device_id"] = torch.device("cuda", local)
+      kw["device_id"] = torch.device("cuda", local_device_index(local))
     dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
   return rank, world, local
 
