@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -40,6 +40,7 @@ _SIGS: dict[str, list] = {
                                 I64, I32, F32, P],
     "cadence_rglru_gates": [P, I64, P, I64, P, P, P, P, P, P, I64, I64, I64, I64,
                             P, I64, P],
+    "cadence_rglru_gates_stream_plan": [P, I64, P, I64, I64, I64, I64],
     "cadence_gemm_rmsnorm_workspace_bytes": [I64, I64, I64],
     "cadence_qkv_rope_decode": [P, I64, P, I64, P, P, P, P, I64, I64, I64, I64, P,
                                 I64, I32, F32, P],

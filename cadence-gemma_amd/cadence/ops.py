@@ -222,23 +222,18 @@ def copy_batched_(pairs) -> None:
 
 
 def claim_counters(stream: torch.cuda.Stream, owner) -> None:
-  """Ties the counter buffer of `stream` to `owner` (a captured decode graph,
-  whose kernels hold its raw pointer): the owner keeps the buffer alive, and
-  the table entry is dropped when the owner is collected, so recaptures on
-  fresh streams do not accumulate buffers.  A stream handle the pool hands
-  out again later gets a fresh zeroed buffer; kernels leave counters at zero
-  and launches on one stream never overlap, so sharing is safe either way."""
-  import weakref
+  """Hands the counter buffer of the capture `stream` over to `owner` (a
+  captured decode graph, whose kernels hold its raw pointer) and removes it
+  from the per-stream table.  The graph is replayed on other streams (a
+  lane, the caller's), while torch's stream pool hands the capture stream's
+  handle out again (32 handles, round robin): an eager launch on that handle
+  must not find the graph's buffer, or its split combines would share
+  arrival counters with a concurrent replay.  After the hand-over the next
+  use of the handle allocates a fresh zeroed buffer."""
   key = (stream.device.index, stream.cuda_stream)
-  buf = _COUNTERS.get(key)
-  if buf is None:
-    return
-  owner._cadence_counters = buf
-
-  def drop(key=key, ref=weakref.ref(buf)):
-    if _COUNTERS.get(key) is ref():
-      _COUNTERS.pop(key, None)
-  weakref.finalize(owner, drop)
+  buf = _COUNTERS.pop(key, None)
+  if buf is not None:
+    owner._cadence_counters = buf
 
 
 def _ws(M: int, N: int, K: int, groups: int, like: torch.Tensor):
@@ -576,8 +571,8 @@ def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos,
       E, M, H, bw, _p(ws), nws,
       _s(x)), "rglru_gates")
   if ev is not None:
-    if (not decode_layout and bw in (64, 128, 256) and
-        _lib.load().cadence_gemm_set_engine(-1) & 2):
+    if _lib.load().cadence_rglru_gates_stream_plan(
+        _p(x), ldx, _p(w_packed), 0 if decode_layout else bw, E, M, bw):
       # the block-bound streaming kernel: priced on HBM bytes (x in, a and
       # normalised x out, the packed weights once)
       TIMER.stop(ev, f"rglru_gates_stream_kernel<{bw}>",

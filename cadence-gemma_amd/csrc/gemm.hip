@@ -2722,7 +2722,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 
 extern "C" {
 
-int cadence_abi_version(void) { return 14; }
+int cadence_abi_version(void) { return 15; }
 
 int cadence_gemm_set_engine(int engine) {
   const int prev = g_engine;
@@ -2996,6 +2996,21 @@ int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
                      norm, norm_eps);
 }
 
+// The prefill gates plan: the block-bound streaming kernel, or (lab switch
+// engine bit 1 clear, a width it has no instance for, packed decode weights,
+// M <= 32, unaligned rows) the block engine's grouped GEMM with EpiRglruGates.
+static bool gates_stream_plan(const void* X, int64_t ldx, const void* Wpacked,
+                              int64_t ldw, int64_t ldo, int64_t M, int64_t bw) {
+  return (g_engine & 2) && ldw == bw && M > 32 && (bw == 64 || bw == 128 || bw == 256) &&
+         ldx % 8 == 0 && ldo % 8 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0 &&
+         reinterpret_cast<uintptr_t>(Wpacked) % 16 == 0;
+}
+
+int cadence_rglru_gates_stream_plan(const void* X, int64_t ldx, const void* Wpacked,
+                                    int64_t ldw, int64_t ldo, int64_t M, int64_t bw) {
+  return gates_stream_plan(X, ldx, Wpacked, ldw, ldo, M, bw) ? 1 : 0;
+}
+
 int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
                         int64_t ldw, const void* bias_x, const void* bias_a,
                         const void* softplus_a, const int32_t* segment_pos,
@@ -3011,9 +3026,7 @@ int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
                     (int)bw, nullptr, 0, nullptr, 0, nullptr, 0, 1};
   hipStream_t st = static_cast<hipStream_t>(stream);
   // (lab switch: engine 0 keeps the block engine, for the bitwise A/B test)
-  if ((g_engine & 2) && ldw == bw && M > 32 && (bw == 64 || bw == 128 || bw == 256) && ldx % 8 == 0 &&
-      ldo % 8 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0 &&
-      reinterpret_cast<uintptr_t>(Wpacked) % 16 == 0) {
+  if (gates_stream_plan(X, ldx, Wpacked, ldw, ldo, M, bw)) {
     // prefill: the block-bound streaming kernel, ~256 / heads workgroups per
     // block (2 / 4 per CU for the narrower blocks' smaller waves counts)
     const int64_t ntiles = (M + 31) / 32;

@@ -206,6 +206,14 @@ int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
                         int64_t heads, int64_t bw, void* workspace,
                         int64_t ws_bytes, void* stream);
 
+/* Plan query (host only, no GPU work): 1 when cadence_rglru_gates with these
+ * operands runs the block-bound streaming kernel (rglru_gates_stream_kernel:
+ * bw in {64, 128, 256}, row-major weights, M > 32, 16-byte aligned X and W,
+ * ldx and ldo multiples of 8), 0 when it runs the block engine's grouped GEMM
+ * with the gate-chain epilogue.  Used to name the kernel a timed launch ran. */
+int cadence_rglru_gates_stream_plan(const void* X, int64_t ldx, const void* Wpacked,
+                                    int64_t ldw, int64_t ldo, int64_t M, int64_t bw);
+
 /* Single-token RG-LRU step (decode, T = 1): the gate GEMM + chain of
  * cadence_rglru_gates with the scan step of rnn_scan's T == 1 branch fused
  * into the epilogue (layers.py:175-182, modules.py:652):

@@ -203,3 +203,25 @@ def test_roctx_ranges_nest():
     tracing.enable(prev)
   assert tracing.enabled() == prev
 
+
+
+def test_rglru_gates_plan_query():
+  """cadence_rglru_gates_stream_plan (host-only): the streaming gates kernel
+  for aligned row-major prefill operands of a width it has, the block engine
+  otherwise (packed decode weights, M <= 32, other widths, odd strides,
+  misaligned rows, or the lab switch's engine bit 1 clear)."""
+  lib = _lib.load()
+  plan = lib.cadence_rglru_gates_stream_plan
+  A, W = 0x10000, 0x20000
+  assert plan(A, 5120, W, 256, 2560, 10208, 256) == 1
+  assert plan(A, 512, W, 64, 512, 100, 64) == 1
+  assert plan(A, 5120, W, 0, 2560, 10208, 256) == 0      # fragment-packed
+  assert plan(A, 5120, W, 256, 2560, 32, 256) == 0       # decode rows
+  assert plan(A, 5120, W, 192, 2560, 10208, 192) == 0    # no instance
+  assert plan(A + 2, 5120, W, 256, 2560, 10208, 256) == 0
+  assert plan(A, 5121, W, 256, 2560, 10208, 256) == 0
+  prev = lib.cadence_gemm_set_engine(0)
+  try:
+    assert plan(A, 5120, W, 256, 2560, 10208, 256) == 0
+  finally:
+    lib.cadence_gemm_set_engine(prev)

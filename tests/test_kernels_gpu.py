@@ -435,14 +435,13 @@ def test_rope_and_local_attention(dev, b, t, h, hd, window, split):
 
 
 @pytest.mark.parametrize("m,h,hd,k", [(32 * 319, 10, 256, 2560), (32 * 639, 10, 256, 2560),
-                                      (300, 4, 128, 512), (1000, 6, 64, 512)])
+                                      (8 * 319, 10, 256, 2560)])
 def test_qkv_rope_prefill_matches_two_launch_form(dev, m, h, hd, k):
   """Prompt-pass q|k|v GEMM with RoPE in the staged epilogue (permuted
   weight rows) == linear on the natural rows, then rope_qkv: bitwise (same
   per-column MFMA chains, same rotation arithmetic).  Positions include
   document resets, -1 padding and positions past the sin / cos table."""
-  if not ops.qkv_rope_prefill_ok(m, h, hd, k):
-    pytest.skip("plan is not one unsplit block-engine launch")
+  assert ops.qkv_rope_prefill_ok(m, h, hd, k), "plan should be one unsplit launch"
   g = torch.Generator().manual_seed(21)
   x = rnd(m, k, gen=g).to(dev)
   w = rnd((h + 2) * hd, k, scale=1 / math.sqrt(k), gen=g).to(dev)
@@ -458,6 +457,55 @@ def test_qkv_rope_prefill_matches_two_launch_form(dev, m, h, hd, k):
   assert torch.equal(v1, v0)
   assert torch.equal(k1, k0)
   assert torch.equal(q1, q0)
+
+
+@pytest.mark.parametrize("m,h,hd,k", [(319, 10, 256, 2560), (300, 4, 128, 512),
+                                      (1000, 6, 64, 512)])
+def test_qkv_split_k_then_rope_path(dev, m, h, hd, k):
+  """The q|k|v path of shapes the fused prefill launch does not cover (C3's
+  B = 1 prompt, M = 319: split-K partial GEMM + reduce, then rope_qkv).
+  The attention block's forward equals the explicit two-launch composition
+  bitwise (so it takes this path and nothing else); the split-K GEMM is
+  within one bf16 rounding of an fp32 matmul (>= 98 % bit-equal), and the
+  rotation of its output matches the oracle's RoPE on the same rows
+  (>= 99.5 % bit-equal: sin / cos rounding)."""
+  from cadence import _lib
+  n = (h + 2) * hd
+  lib = _lib.load()
+  assert not ops.qkv_rope_prefill_ok(m, h, hd, k)
+  g = torch.Generator().manual_seed(22)
+  x = rnd(m, k, gen=g)
+  w = rnd(n, k, scale=1 / math.sqrt(k), gen=g)
+  pos = torch.randint(-1, 3000, (m,), generator=g, dtype=torch.int32)
+  pos[::7] = 0
+  xd, wd, pd = x.to(dev), w.to(dev), pos.to(dev)
+  qkv = ops.linear(xd, wd)
+  want = (x.float() @ w.float().t()).to(BF)
+  assert_close_bf16(qkv, want, rtol=1e-2, atol=1e-2, min_equal=0.98, what="split-K qkv")
+  table = ops.rope_table(dev, hd)
+  q, kk, v = ops.ops.rope_qkv(qkv, pd, h, hd, table)
+  assert torch.equal(v.cpu(), qkv.cpu()[:, (h + 1) * hd:])
+  qc = qkv.cpu()
+  q_ref = R.apply_rope(qc[:, :h * hd].view(1, m, h, hd), pos[None]).view(m, h * hd)
+  k_ref = R.apply_rope(qc[:, h * hd:(h + 1) * hd].view(1, m, 1, hd), pos[None]).view(m, hd)
+  assert_close_bf16(q, q_ref, rtol=1e-2, atol=1e-2, min_equal=0.995, what="rope q")
+  assert_close_bf16(kk, k_ref, rtol=1e-2, atol=1e-2, min_equal=0.995, what="rope k")
+  if h * hd > 2560 or hd != 256:
+    return
+  # the block's own forward at this shape (B = 1, T = m) == the composition
+  blk = cadence.LocalAttentionBlock(h * hd, h, window_size=2048, device=dev, dtype=BF)
+  with torch.no_grad():
+    blk.proj_q.weight.copy_(w[:h * hd])
+    blk.proj_k.weight.copy_(w[h * hd:(h + 1) * hd])
+    blk.proj_v.weight.copy_(w[(h + 1) * hd:])
+  p2 = torch.arange(m, dtype=torch.int32)[None].to(dev)
+  got, _ = blk(xd[None], p2, return_cache=False)
+  q, kk, v = ops.ops.rope_qkv(qkv, p2.view(-1), h, hd, table)
+  seg, start = ops.ops.segment_info(p2)
+  enc = ops.ops.local_attention(q, kk, v, seg, start, 1, m, h, hd, 2048)
+  ref = ops.linear(enc, blk.proj_final.weight, blk.proj_final.bias,
+                   resid=torch.zeros(m, h * hd, dtype=BF, device=dev))
+  assert torch.equal(got.view(m, -1), ref)
 
 
 @pytest.mark.parametrize("b,ctx", [(32, 352), (1, 1500), (2, 2100), (4, 0)])

@@ -308,3 +308,43 @@ def test_generate_many_pipeline_matches_sequential(dev):
             n = int(cw.num_tokens.max())
             a, c = a[:, :n], c[:, :n]
           assert torch.equal(a, c), name
+
+
+def test_decode_graph_counters_not_shared_after_stream_pool_wraps(dev):
+  """A captured decode graph owns its split-combine arrival counters: once
+  torch's stream pool (32 handles, round robin) hands the capture stream's
+  handle out again, an eager launch on it gets a different buffer, and
+  generate_many after the pool wrapped still equals sequential generate
+  (a graph replayed on a lane stream must not share counters
+  with a stream that reuses its capture handle)."""
+  from cadence import ops
+  cfg = small_config(window=64)
+  m, _ = make_model(dev, cfg, seed=41)
+  vocab = MockVocab()
+  g = torch.Generator().manual_seed(42)
+  b, t, steps = 4, 10, 7
+  batches = []
+  for j in range(4):
+    tok = torch.randint(3, cfg.vocab_size, (b, t), generator=g, dtype=torch.int32)
+    batches.append((tok.to(dev), torch.full((b,), t, dtype=torch.int32), None))
+  want = [cadence.Sampler(m, vocab, use_graph=True).generate(tk, ln, steps)
+          for tk, ln, _ in batches]
+  pipe = cadence.Sampler(m, vocab, use_graph=True)
+  pipe.generate_many(batches, steps)
+  owned = {(e.stream.cuda_stream, e._cadence_counters.data_ptr())
+           for e in pipe._graphs.values() if hasattr(e, "_cadence_counters")}
+  assert owned, "decode graphs should own their counter buffers"
+  keep = [torch.cuda.Stream(device=dev) for _ in range(40)]   # wrap the pool
+  reused = 0
+  for s in keep:
+    for handle, ptr in owned:
+      if s.cuda_stream == handle:
+        with torch.cuda.stream(s):
+          buf = ops._counters(torch.device(dev), 64)
+        assert buf.data_ptr() != ptr
+        reused += 1
+  assert reused, "the stream pool never handed a capture handle out again"
+  for _ in range(2):
+    got = pipe.generate_many(batches, steps)
+    for w, gt in zip(want, got):
+      assert torch.equal(w.tokens_buffer.cpu(), gt.tokens_buffer.cpu())
