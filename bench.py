@@ -90,6 +90,12 @@ def parse():
   ap.add_argument("--no-pipeline", action="store_true",
                   help="run the micro-batches back to back (generate per "
                   "micro-batch) instead of Sampler.generate_many's pipeline")
+  ap.add_argument("--split-single", action="store_true",
+                  help="lab: a rank whose share is one micro-batch runs it as "
+                  "two pipelined halves (generate_many) instead of whole; "
+                  "measured slower (profiles/r04c_n8_load_*: 135.7 vs 103.6 "
+                  "ms for 32 samples -- a decode step streams every weight "
+                  "whatever its row count, so two halves stream them twice)")
   ap.add_argument("--gemm-engine", type=int, default=None,
                   help="lab A/B: prefill GEMM engine plan (cadence_gemm_set_engine)")
   args = ap.parse_args()
@@ -130,14 +136,22 @@ def make_inputs(global_batch, lo, hi, image_size, prompt, vocab, text_only):
   return tok[lo:hi].contiguous(), images
 
 
-def shard_plan(global_batch, micro_batch, rank, world):
+def shard_plan(global_batch, micro_batch, rank, world, lanes=1):
   """(lo, hi, micro-batch slices) of the samples `rank` runs: a contiguous
-  block of the global batch, cut into micro-batches of `micro_batch`."""
+  block of the global batch, cut into micro-batches of `micro_batch`.  With
+  `lanes` > 1 (the two-lane generate_many pipeline) a rank whose share is ONE
+  micro-batch runs it as `lanes` equal parts instead, so one part's prefill
+  overlaps another's decode (lab option for the N = 8 point of the
+  256-sample strong-scaling curve, 32 samples per rank: 2 x 16 measured
+  slower than 1 x 32, profiles/r04c_n8_load_*)."""
   lo, hi = D.shard_range(global_batch, rank, world)
   if (hi - lo) % micro_batch:
     raise ValueError(f"{hi - lo} samples per rank is not a multiple of the "
                      f"micro-batch {micro_batch}")
   n = (hi - lo) // micro_batch
+  if n == 1 and lanes > 1 and micro_batch % lanes == 0:
+    micro_batch //= lanes
+    n = lanes
   return lo, hi, [slice(j * micro_batch, (j + 1) * micro_batch) for j in range(n)]
 
 
@@ -341,16 +355,19 @@ def main():
   n_vis = 0 if vis is None else vis.n_visual_tokens
   strong = bool(args.global_batch)
   gb = args.global_batch if strong else args.batch * world
-  lo, hi, micro = shard_plan(gb, args.batch, rank, world)
+  pipelined_plan = bool(args.decode and not args.no_pipeline and args.split_single)
+  lo, hi, micro = shard_plan(gb, args.batch, rank, world,
+                             lanes=2 if pipelined_plan else 1)
   n_micro = len(micro)
+  mb = micro[0].stop - micro[0].start          # samples per micro-batch
   tok_cpu, img_cpu = make_inputs(gb, lo, hi, args.image_size, args.prompt,
                                  cfg.vocab_size, args.text_only)
   tokens = tok_cpu.to(dev)
   images = None if img_cpu is None else img_cpu.to(dev)
-  lengths = torch.full((args.batch,), args.prompt, dtype=torch.int32)
+  lengths = torch.full((mb,), args.prompt, dtype=torch.int32)
   sampler = cadence.Sampler(model, BenchVocab(), use_graph=True)
   positions = torch.arange(args.prompt, dtype=torch.int32, device=dev)[None].repeat(
-      args.batch, 1)
+      mb, 1)
 
   def step(events=None, pipeline=True):
     # (one micro-batch has nothing to overlap: plain Sampler.generate)
@@ -458,7 +475,7 @@ def main():
   ms_step = elapsed / args.steps * 1e3
   pre_ms = sum(prefill_ms) / max(len(prefill_ms), 1)
   pre_ms = D.max_over_ranks(pre_ms)
-  prefill_tps = args.batch * (n_vis + args.prompt - (1 if args.decode else 0)) / (
+  prefill_tps = mb * (n_vis + args.prompt - (1 if args.decode else 0)) / (
       pre_ms * 1e-3)
 
   result = None
@@ -479,7 +496,7 @@ def main():
       # decode steps; step i attends to n_vis + prompt + i keys
       dsteps = ev_list[0]["decode_steps"]
       ctx = [n_vis + args.prompt + i for i in range(args.decode - dsteps, args.decode)]
-      nbytes = decode_hbm_bytes(model, cfg, args.batch, ctx,
+      nbytes = decode_hbm_bytes(model, cfg, mb, ctx,
                                 cfg.attention_window_size)
       us = sum(decode_ms) / len(decode_ms) * 1e3
       gbs = nbytes / (us * 1e-6) / 1e9
@@ -511,10 +528,10 @@ def main():
             "workload": ("Cadence-2B (RecurrentGemma-2B + DINOv2-L/14-reg4 + "
                          "SigLIP-so400m/14 + MLP projector) " + what +
                          f", global batch {gb} = {world} GPU(s) x {n_micro} "
-                         f"micro-batch(es) of {args.batch}, prompt "
+                         f"micro-batch(es) of {mb}, prompt "
                          f"{args.prompt}, greedy decode {args.decode}"),
             "config": args.config,
-            "global_batch": gb, "micro_batch": args.batch,
+            "global_batch": gb, "micro_batch": mb,
             "micro_batches_per_gpu": n_micro,
             "image_size": None if args.text_only else args.image_size,
             "n_visual_tokens": n_vis,

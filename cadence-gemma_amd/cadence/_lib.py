@@ -15,7 +15,9 @@ import threading
 import torch  # noqa: F401  (load torch's HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcadence_hip.so")
+# CADENCE_LIB_PATH: the host-ASan build of the same C-ABI
+# (tools/asan_host.sh, CPU-only contract tests); unset everywhere else
+LIB_PATH = os.environ.get("CADENCE_LIB_PATH") or os.path.join(_HERE, "libcadence_hip.so")
 ABI_VERSION = 15
 
 _lock = threading.Lock()

@@ -29,6 +29,9 @@ int griffin_attention_launch(const void* q, const void* k, const void* v,
                              void* stream);  // griffin_attention.hip
 int vit_stream_attention_launch(const void* qkv, void* out, int64_t B, int64_t N,
                                 int64_t H, int64_t hd, void* stream);
+int vit_flash_attention_launch(const void* qkv, void* out, int64_t B, int64_t N,
+                               int64_t H, int64_t hd, void* stream);  // vit_flash.hip
+int cadence_engine_bits();                                            // gemm.hip
 int generic_attention_launch(const void* q, const void* k, const void* v,
                              const void* cache_k, const void* cache_v,
                              const int32_t* num_tokens, const int32_t* seg_start,
@@ -811,6 +814,14 @@ int cadence_vit_attention(const void* qkv, void* out, int64_t B, int64_t N,
                           int64_t H, int64_t hd, void* stream) {
   if (hd != 64 && hd != 72) return (int)hipErrorInvalidValue;
   if (B <= 0 || N <= 0) return 0;
+  // the streaming kernel with MFMA-computed softmax sums (vit_flash.hip) for
+  // every shape but DINO's 224-px one (N = 261, hd 64), where the
+  // LDS-resident kernel is faster (25.7 vs 29.2 us at bs 32; SigLIP 224 px
+  // 24.4 vs 28.7, 336 px 78 / 86 vs 97 / 112: profiles/r04g_vit_flash_ab.log)
+  if ((cadence_engine_bits() & 8) && !(hd == 64 && N <= 288)) {
+    const int rc = vit_flash_attention_launch(qkv, out, B, N, H, hd, stream);
+    if (rc >= 0) return rc;
+  }
   // LDS-resident swapped-QK^T kernel (vit_attention.hip) for short sequences
   {
     const int rc = vit_attention_lds_launch(qkv, out, B, N, H, hd, stream);

@@ -2466,9 +2466,11 @@ void launch_stream(const u16* A, int64_t lda, const u16* W, int64_t ldw,
 
 // lab A/B switch of the prefill engines, a bit mask: bit 0 = the 4-wave
 // gemm_w4_kernel on its plans, bit 1 = rglru_gates_stream_kernel, bit 2 =
-// the residual-prefetching linear epilogue EpiLinearA<4> (0 = the 8-wave
-// block engine with the plain epilogues for everything)
-int g_engine = 7;
+// the residual-prefetching linear epilogue EpiLinearA<4>, bit 3 = the
+// streaming ViT attention kernel vit_flash_attn_kernel for every tower size
+// (0 = the 8-wave block engine with the plain epilogues for everything, and
+// the round-3 ViT attention kernels)
+int g_engine = 15;
 
 // The 4-wave engine runs the wide long-K GEMMs (the gated MLP up-projection,
 // N = 2F = 15360, K = 2560) on 224 / 256-row tile plans.  Measured A/B in
@@ -2719,6 +2721,9 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
 }
 
 }  // namespace
+
+// the lab switch's bits for the other translation units (attention.hip)
+__attribute__((visibility("hidden"))) int cadence_engine_bits() { return g_engine; }
 
 extern "C" {
 

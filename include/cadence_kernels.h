@@ -92,13 +92,16 @@ int cadence_gemm_big_splits(int64_t M, int64_t N, int64_t K, int64_t groups);
  * decode engines).  Host-side plan query. */
 int cadence_gemm_engine(int64_t M, int64_t N, int64_t K, int64_t groups);
 
-/* Lab A/B switch of the prefill engines, a bit mask (default 7): bit 0 =
+/* Lab A/B switch of the prefill engines, a bit mask (default 15): bit 0 =
  * the 4-wave gemm_w4_kernel for K >= 2048 on 224 / 256-row tile plans (else
  * the 8-wave gemm_big_kernel), bit 1 = prefill RG-LRU gates of 64 / 128 /
  * 256-wide blocks on rglru_gates_stream_kernel, bit 2 = the linear GEMM with
  * a residual loads its residual rows ahead of the staged epilogue (same
- * bits); 0 = the 8-wave block engine with the plain epilogues for everything.  A negative value only queries.  Returns the previous
- * value.  Host state only. */
+ * bits), bit 3 = cadence_vit_attention on the streaming kernel with
+ * MFMA-computed softmax sums for every sequence length (else the LDS-resident
+ * kernel up to 288 tokens and the round-3 streaming kernel above); 0 = the
+ * 8-wave block engine with the plain epilogues for everything.  A negative
+ * value only queries.  Returns the previous value.  Host state only. */
 int cadence_gemm_set_engine(int engine);
 
 /* ---- GEMMs with fused epilogues ---------------------------------------- */

@@ -55,11 +55,11 @@ N_FEATURE_ROWS = 24
 # the only size the reference itself accepts (griffin.py:186-191).
 CONFIGS = {
     "c1": (None, 1, 16, 8, 101),
-    "c2": (None, 1, 2048, 4, 101),
+    "c2": (None, 1, 2048, 8, 101),
     "c3": (224, 1, 64, 8, 202),
-    "bench224": (224, 2, 64, 4, 202),
-    "c4": (336, 1, 64, 4, 303),
-    "p0": (384, 1, 16, 4, 404),
+    "bench224": (224, 2, 64, 8, 262),
+    "c4": (336, 1, 64, 8, 313),
+    "p0": (384, 1, 16, 8, 434),
 }
 
 

@@ -22,7 +22,8 @@ def _same(outs, what):
 
 
 @pytest.mark.parametrize("b,n,h,hd", [(32, 261, 16, 64), (32, 256, 16, 72),
-                                      (4, 581, 16, 64), (4, 729, 16, 72)])
+                                      (4, 581, 16, 64), (4, 729, 16, 72),
+                                      (32, 581, 16, 64), (32, 576, 16, 72)])
 def test_vit_attention_deterministic(dev, b, n, h, hd):
   g = torch.Generator().manual_seed(3)
   qkv = torch.randn(b * n, 3 * h * hd, generator=g).to(BF).to(dev)

@@ -118,6 +118,12 @@ def test_bench_shard_plan():
   assert (lo, hi, len(sl)) == (128, 256, 4)
   with pytest.raises(ValueError):
     bench.shard_plan(256, 48, 0, 2)
+  # two pipeline lanes: a rank with one micro-batch runs it as two halves,
+  # covering the same contiguous rows; ranks with several are unchanged
+  lo, hi, sl = bench.shard_plan(256, 32, 7, 8, lanes=2)
+  assert (lo, hi, sl) == (224, 256, [slice(0, 16), slice(16, 32)])
+  assert bench.shard_plan(256, 32, 1, 4, lanes=2)[2] == [slice(0, 32), slice(32, 64)]
+  assert bench.shard_plan(256, 32, 0, 1, lanes=2)[2] == bench.shard_plan(256, 32, 0, 1)[2]
 
 
 def test_shard_range_contract():

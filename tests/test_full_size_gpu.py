@@ -8,28 +8,41 @@ values are compared exactly) and checked against the CPU oracle's outputs
 committed by tests/golden/make_golden_full.py:
 
   c1        text-only, B=1, T=16, 8 decode steps   (BASELINE config 1's shape)
-  c2        text-only, B=1, T=2048, 4 steps        (config 2's prompt length)
+  c2        text-only, B=1, T=2048, 8 steps        (config 2's prompt length)
   c3        224 px, B=1, T=64, 8 steps             (config 3)
-  bench224  224 px, B=2, T=64, 4 steps             (the bench workload per sample)
-  c4        336 px, B=1, T=64, 4 steps             (config 4; ViT N = 581 / 576)
-  p0        384 px, B=1, T=16, 4 steps             (the reference's own size, n_vis 729)
+  bench224  224 px, B=2, T=64, 8 steps             (the bench workload per sample)
+  c4        336 px, B=1, T=64, 8 steps             (config 4; ViT N = 581 / 576)
+  p0        384 px, B=1, T=16, 8 steps             (the reference's own size, n_vis 729)
+
+The fixture weights (hashinit.param_spec) put the residual projections at
+5 / sqrt(fan_in) and the tied embedding at 1.5 / sqrt(D), so the blocks,
+not the input token's own embedding, decide the logits: greedy
+continuations vary (>= 3 distinct tokens per row, checked on the CPU by
+tests/test_full_fixtures_cpu.py) with top-1 / top-2 margins of a fraction of
+a logit to a few logits, and the teacher-forced decode feeds changing tokens.
 
 Bars: vision features rel-L2 <= 1e-2 against the fp32 towers
 (bf16 MFMA, fp32 residual stream), projector rel-L2 <= 2e-2; logits of the
 prefill forward's last position and of every teacher-forced decode step
 (the oracle's greedy tokens fed back, examples/cadence_sampler.py:185-298),
 on the oracle's top-256 + 4096 fixed vocabulary entries:
-  * cosine >= 0.999 against the bf16 oracle;
+  * against the bf16 oracle: cosine >= 0.999 -- or, where the oracle's own
+    cosine to the fp32 run is 1 - e with 2e > 0.001, >= 1 - 2e (two bf16
+    pipelines each e from fp32); max-abs at most max(0.25, 2x the oracle's
+    own max-abs distance from fp32);
   * accuracy against an fp32 run of the same op sequence (`logit_val_fp32`,
     make_golden_full.add_fp32): max-abs and rel-L2 of the HIP path's error
     at most 1.25x the bf16 oracle's own error (+0.02 / +0.005).  SURVEY's
     "max-abs <= 0.1 vs the reference" cannot be the bar: the reference's own
-    bf16 arithmetic is 0.10-0.15 from fp32 on these logits (printed by
+    bf16 arithmetic is 0.25-0.7 from fp32 on these logits (printed by
     make_golden_full.py), and two bf16 pipelines of that accuracy differ by
-    up to twice that; so max-abs vs the bf16 oracle is capped at 0.25;
-  * greedy token equal wherever the oracle's top-1/top-2 margin exceeds 0.2
-    (else within the oracle's top 2);
-the hipGraph sampler's tokens equal the oracle's greedy tokens.
+    up to twice that;
+  * greedy token equal wherever the oracle's top-1/top-2 margin exceeds the
+    larger of 0.2 and 1.5x the oracle's own max-abs distance from fp32 on
+    that row (else within the oracle's top 2);
+the hipGraph sampler's tokens equal the oracle's greedy tokens up to the
+first step whose margin is within that bar (there: one of the oracle's top
+2; the continuations may part after it).
 """
 
 import json
@@ -94,6 +107,14 @@ def _build(name, dev, f, meta):
   return m, cfg, vis
 
 
+def _margin_bar(f, i, j):
+  """The top-1 / top-2 margin above which the oracle's choice is decided by
+  the reference arithmetic rather than its bf16 noise: MARGIN, or 1.5x the
+  oracle's own max-abs distance from the fp32 run on that row."""
+  d = float((f["logit_val"][i, j] - f["logit_val_fp32"][i, j]).abs().max())
+  return max(MARGIN, 1.5 * d)
+
+
 def _check_row(got, f, i, j, what, bad):
   """got: [V] logits of sample i, fixture row j (0 = prefill last position,
   1 + s = decode step s).  Violations go to `bad` (reported together)."""
@@ -105,13 +126,18 @@ def _check_row(got, f, i, j, what, bad):
   d = (sub - want).abs()
   err = float(d.max())
   w = int(d.argmax())
-  if c < COS:
-    bad.append(f"{what}: cosine {c:.6f}")
-  if err > MAX_ABS:
-    bad.append(f"{what}: max-abs {err:.4f} vs the bf16 oracle at want "
-               f"{float(want[w]):.4f} got {float(sub[w]):.4f}")
+  # two pipelines each (1 - c_ref) from fp32 in cosine are up to about
+  # twice that apart: the bar is COS unless the oracle itself is further
+  cos_bar = min(COS, 1.0 - 2.0 * (1.0 - cosine(want, exact)))
+  if c < cos_bar:
+    bad.append(f"{what}: cosine {c:.6f} (bar {cos_bar:.6f})")
   ours = float((sub - exact).abs().max())
   ref = float((want - exact).abs().max())
+  # two bf16 pipelines each `ref` from fp32 differ by up to about twice it
+  if err > max(MAX_ABS, 2.0 * ref):
+    bad.append(f"{what}: max-abs {err:.4f} vs the bf16 oracle (bar "
+               f"{max(MAX_ABS, 2.0 * ref):.4f}) at want {float(want[w]):.4f} got "
+               f"{float(sub[w]):.4f}")
   ours_l2, ref_l2 = rel_l2(sub, exact), rel_l2(want, exact)
   if ours > ACC * ref + 0.02:
     bad.append(f"{what}: max-abs vs fp32 {ours:.4f}, bf16 oracle's own {ref:.4f}")
@@ -120,14 +146,40 @@ def _check_row(got, f, i, j, what, bad):
                f"{ref_l2:.5f}")
   top2 = idx[torch.topk(want, 2).indices]
   am = int(got.float().argmax())
-  if float(f["logit_margin"][i, j]) > MARGIN:
+  if float(f["logit_margin"][i, j]) > _margin_bar(f, i, j):
     if am != int(top2[0]):
       bad.append(f"{what}: argmax {am} vs {int(top2[0])}")
   elif am not in top2.tolist():
     bad.append(f"{what}: argmax {am} not in oracle top-2")
-  return {"cos": round(c, 6), "max_abs_vs_oracle": round(err, 4),
+  return {"cos": round(c, 6), "cos_bar": round(cos_bar, 6),
+          "max_abs_vs_oracle": round(err, 4),
           "max_abs_vs_fp32": round(ours, 4), "oracle_max_abs_vs_fp32": round(ref, 4),
           "rel_l2_vs_fp32": round(ours_l2, 5), "oracle_rel_l2_vs_fp32": round(ref_l2, 5)}
+
+
+def _check_tokens(got, f, i, what, bad):
+  """A sampler's greedy tokens `got` [S] against the oracle's for fixture
+  sample i, step by step: equal while the oracle's top-1 / top-2 margin
+  exceeds _margin_bar; at a step whose margin does not, the token must be one of
+  the oracle's top 2, and where it is the other one the two continuations
+  may legitimately part (the later steps are not compared).  Returns the
+  number of steps compared."""
+  want = f["greedy_tokens"][i]
+  for s in range(want.numel()):
+    g, w = int(got[s]), int(want[s])
+    if float(f["logit_margin"][i, 1 + s]) > _margin_bar(f, i, 1 + s):
+      if g != w:
+        bad.append(f"{what}: sampler token {s} is {g}, oracle {w} "
+                   f"(tokens {got.tolist()} vs {want.tolist()})")
+        return s
+      continue
+    idx = f["logit_idx"][i, 1 + s].long()
+    top2 = idx[torch.topk(f["logit_val"][i, 1 + s], 2).indices].tolist()
+    if g not in top2:
+      bad.append(f"{what}: sampler token {s} is {g}, not in the oracle's top 2 {top2}")
+    if g != w:
+      return s + 1
+  return want.numel()
 
 
 @pytest.mark.parametrize("name", list(MG.CONFIGS))
@@ -173,10 +225,12 @@ def test_full_size_parity(dev, name):
                                              bad)
       cur, p = gt[:, s:s + 1], p + 1
   # the graph-replayed sampler reproduces the oracle's greedy continuation
-  ok = bool((f["logit_margin"][:, 1:] > MARGIN).all())
   st = cadence.Sampler(m, _Vocab()).generate(
       tok, torch.full((b,), t, dtype=torch.int32), steps, images=px)
-  if ok and not torch.equal(st.tokens_buffer.cpu(), f["greedy_tokens"]):
-    bad.append(f"{name}: sampler tokens {st.tokens_buffer.tolist()}")
+  got = st.tokens_buffer.cpu()
+  for i in range(b):
+    report[f"sampler[{i}]"] = {
+        "steps_compared": _check_tokens(got[i], f, i, f"{name} row {i}", bad),
+        "distinct_oracle_tokens": len(set(f["greedy_tokens"][i].tolist()))}
   print(name, json.dumps(report), flush=True)
   assert not bad, "\n".join(bad)

@@ -17,7 +17,8 @@ Rows 0 and 31 are held to the bars of tests/test_full_size_gpu.py:
     185-298 per row, i.e. the reference's B = 1 semantics
     (recurrentgemma/torch/griffin.py:171-172) row by row;
   * the graph sampler's tokens (Sampler.generate, exactly as bench.py calls
-    it) equal the oracle's greedy tokens.
+    it) equal the oracle's greedy tokens (up to the first step the oracle
+    itself decides within a 0.2-logit margin).
 
 Batches: bench224 (224 px, the bench's per-sample workload), c4 (336 px),
 c2 (text-only, T = 2048).
@@ -37,7 +38,7 @@ import make_golden_full as MG  # noqa: E402
 
 import cadence  # noqa: E402
 from cadence import _lib, ops  # noqa: E402
-from test_full_size_gpu import MARGIN, _Vocab, _build, _check_row, _fixture  # noqa: E402
+from test_full_size_gpu import _Vocab, _build, _check_row, _check_tokens, _fixture  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 B = 32
@@ -114,13 +115,10 @@ def test_headline_batch_parity(dev, name):
       p = p + 1
     del cache
   # the bench's own call: Sampler.generate with the captured decode graph
-  ok = bool((f["logit_margin"][:, 1:] > MARGIN).all())
   st = cadence.Sampler(m, _Vocab()).generate(
       tok, torch.full((B,), t, dtype=torch.int32), steps, images=px)
   got = st.tokens_buffer.cpu()
   for r, j in zip(ROWS, src):
-    if ok and not torch.equal(got[r], f["greedy_tokens"][j]):
-      bad.append(f"{name} B=32 sampler row {r}: {got[r].tolist()} vs "
-                 f"{f['greedy_tokens'][j].tolist()}")
+    report[f"sampler[{r}]"] = _check_tokens(got[r], f, j, f"{name} B=32 row {r}", bad)
   print(name, "B=32", json.dumps(report), flush=True)
   assert not bad, "\n".join(bad)

@@ -593,10 +593,14 @@ def test_kv_cache_fill_and_decode(dev):
 
 @pytest.mark.parametrize("n,h,hd", [(261, 16, 64), (256, 16, 72), (40, 2, 72),
                                     (581, 16, 64), (576, 16, 72), (734, 16, 64),
-                                    (729, 16, 72), (300, 3, 72), (289, 2, 64)])
+                                    (729, 16, 72), (300, 3, 72), (289, 2, 64),
+                                    (1, 2, 72), (64, 3, 72), (65, 2, 72), (320, 2, 64),
+                                    (385, 1, 64), (129, 5, 72)])
 def test_vit_attention(dev, n, h, hd):
-  """timm SDPA (fp32) vs the LDS-resident kernel (N <= 288) and the
-  streaming kernel (336 / 384 px towers: DINO 581 / 734, SigLIP 576 / 729)."""
+  """timm SDPA (fp32) vs the LDS-resident kernel (hd 64, N <= 288) and the
+  streaming kernel vit_flash_attn_kernel (everything else: SigLIP 224 px,
+  the 336 / 384 px towers DINO 581 / 734, SigLIP 576 / 729; tails of 1, 5,
+  33 keys and whole tiles; query blocks of 1 to 8 tiles)."""
   g = torch.Generator().manual_seed(11)
   b = 2
   qkv = rnd(b * n, 3 * h * hd, gen=g)
@@ -721,3 +725,33 @@ def test_copy_batched_matches_tensor_copies(dev):
   torch.cuda.synchronize()
   for dst, w in want:
     assert torch.equal(dst.cpu(), w.cpu())
+
+
+@pytest.mark.parametrize("m", [10208, 4500, 300])
+def test_gemm_w4_engine_bitwise_vs_8wave(dev, m):
+  """The 4-wave prefill engine (gemm_w4_kernel, planned for K >= 2048 and
+  N >= 8192) against the 8-wave block engine it replaced (lab switch engine
+  0), bitwise: linear, linear + bias + residual (the residual-prefetch
+  epilogue, engine bit 2) and the gated-GELU pair epilogue, at the gated
+  MLP's N = 15360, K = 2560, with ragged 224 / 256-row tails."""
+  from cadence import _lib
+  lib = _lib.load()
+  n, k = 15360, 2560
+  g = torch.Generator().manual_seed(23)
+  a = rnd(m, k, gen=g).to(dev)
+  w = rnd(n, k, scale=1 / math.sqrt(k), gen=g).to(dev)
+  bias = rnd(n, scale=0.1, gen=g).to(dev)
+  resid = rnd(m, n, gen=g).to(dev)
+  bg, bu = rnd(n // 2, scale=0.1, gen=g).to(dev), rnd(n // 2, scale=0.1, gen=g).to(dev)
+  runs = {}
+  for eng in (7, 0):
+    prev = lib.cadence_gemm_set_engine(eng)
+    try:
+      runs[eng] = (ops.linear(a, w), ops.linear(a, w, bias, resid=resid),
+                   ops.gated_gelu(a, w, bg, bu))
+    finally:
+      lib.cadence_gemm_set_engine(prev)
+  if m > 4096:
+    assert lib.cadence_gemm_engine(m, n, k, 1) == 1, "the plan should take gemm_w4_kernel"
+  for what, x, y in zip(("linear", "linear+residual", "gated"), runs[7], runs[0]):
+    assert torch.equal(x, y), what
