@@ -252,7 +252,7 @@ def vit_attention_isolated(vis, batch, dev, reps=20):
     nbytes = batch * n * (3 * c.width + c.width) * 2
     t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
     t_mfma = flops / (MFMA_BF16_PEAK_TFS * 1e12)
-    out[c.name] = {"kernel": f"vit_attn_kernel<hd{c.head_dim}>", "bound": "mfma",
+    out[c.name] = {"kernel": ops.vit_attention_kernel_name(n, c.head_dim), "bound": "mfma",
                    "achieved": round(tf, 2), "peak": MFMA_BF16_PEAK_TFS,
                    "unit": "TFLOP/s", "frac": round(tf / MFMA_BF16_PEAK_TFS, 4),
                    "avg_us": round(us, 2), "work_per_launch": flops,
@@ -563,7 +563,8 @@ def main():
         "roofline_by_kernel": {k: roofline_entry(ksum, k, "mfma", args.config)
                                for k in sorted(ksum)
                                if k.startswith(("gemm_big", "gemm_w4", "vit_attn",
-                                                "flash_attn", "griffin_attn"))},
+                                                "vit_flash", "vit_stream", "flash_attn",
+                                                "griffin_attn"))},
         # a seeded 1/sample of the launches is event-timed (TIMER.sample)
         "kernels": {k: {"launches_timed": v["launches"],
                         "avg_us": round(v["avg_ms"] * 1e3, 2),

@@ -82,6 +82,7 @@ _SIGS: dict[str, list] = {
     "cadence_im2col_normalize": [P, P, I64, I64, I64, I64, P, P, P],
     "cadence_vit_prefix": [P, P, I64, I64, I64, I64, P],
     "cadence_vit_attention": [P, P, I64, I64, I64, I64, P],
+    "cadence_vit_attention_kernel": [I64, I64],
     "cadence_vit_features": [P, P, I64, I64, I64, I64, I64, I64, P],
     "cadence_resize_bicubic": [P, I64, P, I64, I64, I64, I64, I64, P, P, I64, P,
                                P],

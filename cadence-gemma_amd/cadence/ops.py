@@ -1086,9 +1086,16 @@ def _vit_attention(qkv, B, N, H, hd):
   ev = TIMER.start(qkv)
   _lib.check(_lib.load().cadence_vit_attention(
       _p(qkv), _p(out), B, N, H, hd, _s(qkv)), "vit_attention")
-  TIMER.stop(ev, f"vit_attn_kernel<hd{hd}>", 4.0 * B * H * N * N * hd,
-             qkv)
+  TIMER.stop(ev, vit_attention_kernel_name(N, hd), 4.0 * B * H * N * N * hd, qkv)
   return out
+
+
+def vit_attention_kernel_name(N: int, hd: int) -> str:
+  """The rocprof name (template arguments folded into hd) of the kernel
+  cadence_vit_attention runs for this shape (host-side plan query)."""
+  k = _lib.load().cadence_vit_attention_kernel(N, hd)
+  return {0: "vit_attn_kernel", 1: "vit_stream_attn_kernel",
+          2: "vit_flash_attn_kernel"}.get(k, "vit_attention?") + f"<hd{hd}>"
 
 
 @_reg("vit_features_(Tensor resid, Tensor(a!) out, int col_off, int B, "

@@ -810,15 +810,26 @@ int cadence_local_attention(const void* q, const void* k, const void* v,
   return (int)hipGetLastError();
 }
 
+// The ViT attention plan: the streaming kernel with MFMA-computed softmax
+// sums (vit_flash.hip) for every shape but DINO's 224-px one (N = 261, hd
+// 64), where the LDS-resident kernel is faster (25.7 vs 29.2 us at bs 32;
+// SigLIP 224 px 24.4 vs 28.7, 336 px 78 / 86 vs 97 / 112:
+// profiles/r04g_vit_flash_ab.log); with the lab switch's bit 3 clear, the
+// round-3 kernels (LDS-resident up to 288 tokens, streaming above).
+static int vit_plan(int64_t N, int64_t hd) {
+  if ((hd != 64 && hd != 72) || N <= 0) return -1;
+  if ((cadence_engine_bits() & 8) && !(hd == 64 && N <= 288)) return 2;
+  if (N <= 288) return 0;
+  return 1;
+}
+
+int cadence_vit_attention_kernel(int64_t N, int64_t hd) { return vit_plan(N, hd); }
+
 int cadence_vit_attention(const void* qkv, void* out, int64_t B, int64_t N,
                           int64_t H, int64_t hd, void* stream) {
   if (hd != 64 && hd != 72) return (int)hipErrorInvalidValue;
   if (B <= 0 || N <= 0) return 0;
-  // the streaming kernel with MFMA-computed softmax sums (vit_flash.hip) for
-  // every shape but DINO's 224-px one (N = 261, hd 64), where the
-  // LDS-resident kernel is faster (25.7 vs 29.2 us at bs 32; SigLIP 224 px
-  // 24.4 vs 28.7, 336 px 78 / 86 vs 97 / 112: profiles/r04g_vit_flash_ab.log)
-  if ((cadence_engine_bits() & 8) && !(hd == 64 && N <= 288)) {
+  if (vit_plan(N, hd) == 2) {
     const int rc = vit_flash_attention_launch(qkv, out, B, N, H, hd, stream);
     if (rc >= 0) return rc;
   }

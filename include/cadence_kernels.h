@@ -423,6 +423,12 @@ int cadence_im2col_normalize(const float* pixels, void* patches, int64_t ldp,
 int cadence_vit_prefix(const void* tokens, float* resid, int64_t B,
                        int64_t ntok, int64_t prefix, int64_t D, void* stream);
 
+/* Plan query (host only): the kernel cadence_vit_attention runs for N
+ * tokens of head dim hd -- 0 the LDS-resident vit_attn_kernel, 1 the
+ * round-3 streaming vit_stream_attn_kernel, 2 vit_flash_attn_kernel (the
+ * streaming kernel with MFMA-computed softmax sums), -1 unsupported. */
+int cadence_vit_attention_kernel(int64_t N, int64_t hd);
+
 /* Bidirectional multi-head attention (timm Attention, fused SDPA):
  * qkv [B*N, 3*H*hd] bf16 -> out [B*N, H*hd] bf16; hd in {64, 72}; qkv and
  * out 16-B aligned (returns hipErrorInvalidValue otherwise). */

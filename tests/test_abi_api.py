@@ -225,3 +225,21 @@ def test_rglru_gates_plan_query():
     assert plan(A, 5120, W, 256, 2560, 10208, 256) == 0
   finally:
     lib.cadence_gemm_set_engine(prev)
+
+
+def test_vit_attention_plan_query():
+  """cadence_vit_attention_kernel (host-only): DINO's 224-px shape on the
+  LDS-resident kernel, every other tower shape on vit_flash_attn_kernel, the
+  round-3 kernels with the lab switch's bit 3 clear."""
+  lib = _lib.load()
+  plan = lib.cadence_vit_attention_kernel
+  assert plan(261, 64) == 0
+  assert [plan(n, hd) for n, hd in ((256, 72), (581, 64), (576, 72), (734, 64), (729, 72))] \
+      == [2] * 5
+  assert plan(100, 80) == -1
+  prev = lib.cadence_gemm_set_engine(-1)
+  lib.cadence_gemm_set_engine(prev & ~8)
+  try:
+    assert (plan(256, 72), plan(581, 64)) == (0, 1)
+  finally:
+    lib.cadence_gemm_set_engine(prev)
