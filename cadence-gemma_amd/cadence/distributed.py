@@ -34,11 +34,15 @@ def local_device_index(local: int) -> int:
 
 
 def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
-  """(rank, world, local rank); joins the process group when world > 1.
-  Backend: `backend`, else $CADENCE_DIST_BACKEND, else "nccl" (RCCL) on a
-  GPU host and "gloo" on CPU."""
+  """(rank, world, local rank); joins the process group when world > 1
+  (or, with CADENCE_DIST_FORCE=1, also as the single rank of a world of one:
+  the RCCL rehearsal on a one-GPU box).  Backend: `backend`, else
+  $CADENCE_DIST_BACKEND, else "nccl" (RCCL) on a GPU host and "gloo" on
+  CPU."""
   rank, world, local = env_world()
-  if world > 1 and not dist.is_initialized():
+  force = os.environ.get("CADENCE_DIST_FORCE") == "1"
+  if (world > 1 or force) and not dist.is_initialized():
+    os.environ.setdefault("MASTER_PORT", "29517")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
       backend = os.environ.get("CADENCE_DIST_BACKEND") or (
