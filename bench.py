@@ -405,6 +405,8 @@ def main():
       outs.append(st.tokens_buffer)
     return D.gather_rows(torch.cat(outs))
 
+  host_enqueue = {}
+
   def timed_pass(kernel_timing: bool):
     """K steps between barrier + synchronize; with kernel_timing a seeded
     1/4 of the prefill GEMM / attention / scan launches carry HIP events on
@@ -429,6 +431,9 @@ def main():
       o = step(ev, pipeline=not kernel_timing)
       sev[i + 1].record()
       evs.append(ev)
+    # host time to enqueue the K steps (no sync inside a step): under the
+    # device time means the host runs ahead and the GPU does not wait on it
+    host_enqueue["s"] = time.perf_counter() - t0
     torch.cuda.synchronize()
     D.barrier()
     t1 = time.perf_counter()
@@ -442,6 +447,7 @@ def main():
     # the headline pass carries no per-kernel events (they cost the stream
     # ~3 % of the step); a second pass of the same K steps times the kernels
     dt, step_ev, ev_list, out = timed_pass(False)
+    host_ms = host_enqueue["s"] * 1e3 / args.steps
     ksum = {}
     pipelined = bool(args.decode and not args.no_pipeline and n_micro > 1)
     if not args.no_kernel_timing:
@@ -518,6 +524,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
         "ms_per_step_median": round(median_ms, 3),
+        "host_enqueue_ms_per_step": round(host_ms, 3),
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,

@@ -58,6 +58,14 @@ class SamplerOutput(NamedTuple):
   tokens: list[torch.Tensor]
 
 
+def _to_device(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
+  """A host tensor on `dev` without blocking the host (pinned staging; the
+  caching host allocator keeps the block until the copy has run)."""
+  if dev.type != "cuda" or t.is_cuda:
+    return t.to(dev)
+  return t.pin_memory().to(dev, non_blocking=True)
+
+
 def prompt_positions(lengths: torch.Tensor, prompt_length: int) -> torch.Tensor:
   """examples/cadence_sampler.py:198-201."""
   pos = torch.arange(prompt_length, dtype=torch.int32)[None].repeat(
@@ -139,7 +147,10 @@ class Sampler:
         raise ValueError(f"prompt token ids must lie in [0, {self.vocab_size}); "
                          f"got [{lo}, {hi}]")
     pos_cpu = prompt_positions(input_lengths.cpu(), t)
-    positions = pos_cpu.to(dev)
+    # host -> device through pinned memory, asynchronous: a pageable copy
+    # blocks the host until the stream has drained, so with two lanes the
+    # host could not enqueue micro-batch j + 2 before j had finished
+    positions = _to_device(pos_cpu, dev)
     # image tokens spliced in front by the prefill (griffin.py:179: only when
     # the prompt holds a position 0); known on the host, so the decode graph
     # copies only the attention-cache slots the prefill wrote
@@ -149,7 +160,8 @@ class Sampler:
     splice = bool((pos_cpu[:, :-1] == 0).any()) if t > 1 else splice_all
     if (images is not None or img_path) and model_vis is not None and splice:
       n_img = self.model.n_visual_tokens
-    tokens = tokens.to(dev, torch.int32)
+    tokens = (tokens.to(dev, torch.int32) if tokens.is_cuda else
+              _to_device(tokens.to(torch.int32), dev))
     steps = total_generation_steps
     # the reference's torch.equal(next_token, eos) only ever holds for B == 1
     eos_stop = end_sampling_at_eos_token and (self.eos_per_row or b == 1)
