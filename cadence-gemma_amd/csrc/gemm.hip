@@ -1713,18 +1713,18 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
 // (tools/gemv_lab2.hip): 6.45-6.52 us against 6.98-7.06 for the 2-split
 // stream kernel with its in-kernel combine; the 39 MB down projection stays on
 // the split engine (per-CU bound unsplit: 15 us against 11.3).
-template <int NW, int KSW, int CH, int INF>
+template <int NW, int KSW, int CH, int INF, int MR>
 __global__ __launch_bounds__(NW * 64) void gemm_resid_pipe_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, int M, int K, EpiResidRows epi) {
-  constexpr int MR = 2, NC = KSW / CH;
-  static_assert(KSW % CH == 0 && INF <= NC && NW * 64 >= 32 * 16, "chunking / epilogue");
-  __shared__ float red[NW][32 * 16];
+  constexpr int NC = KSW / CH, MS = 16 * MR;     // MR 16-row tiles of packed rows
+  static_assert(KSW % CH == 0 && INF <= NC && NW * 64 >= MS * 16, "chunking / epilogue");
+  __shared__ float red[NW][MS * 16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const u16* zpage = reinterpret_cast<const u16*>(kZeroPage + lane);
   const int ks32 = K >> 5;
   const int col0 = blockIdx.x * 16;
   // epilogue operands first: thread t < 512 owns (row t / 16, column t % 16)
-  const int pm = min((int)(threadIdx.x >> 4) & 31, M - 1);
+  const int pm = min((int)(threadIdx.x >> 4) & (MS - 1), M - 1);
   const EpiResidRows::Pref pf = epi.prefetch(pm, col0 + (threadIdx.x & 15));
   uint4 wb[INF][CH], xa[INF][CH][MR];
   auto issue = [&](int c, int slot) {
@@ -1765,7 +1765,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_resid_pipe_kernel(
     for (int r = 0; r < 4; ++r) red[wave][(i * 16 + rsub + r) * 16 + csub] = acc[i][r];
   __syncthreads();
   const int o = threadIdx.x;
-  if (o >= 32 * 16) return;
+  if (o >= MS * 16) return;
   const int m = o >> 4;
   if (m >= M) return;
   float v = 0.f;
@@ -1785,11 +1785,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_resid_pipe_kernel(
 // loads to their first use).  Cold-weight lab (tools/gemv_lab.hip): 17.2 ->
 // 14.0 us on the 2F = 15360, K = 2560 shape.  Same products and fixed-order
 // LDS reduction as gemm_stream_kernel; NORM as there.
-template <int KSW, int CH, int INF, bool NORM>
+template <int KSW, int CH, int INF, bool NORM, int MR>
 __global__ __launch_bounds__(512) void gemm_gated_pipe_kernel(
     const u16* __restrict__ A, const u16* __restrict__ W, int M, int K,
     EpiGatedGelu epi, float neps) {
-  constexpr int MS = 32, MR = 2, NREP = 4, NC = KSW / CH;
+  constexpr int MS = 16 * MR, NREP = 4, NC = KSW / CH;   // MR 16-row tiles
   static_assert(KSW % CH == 0 && INF <= NC, "chunking");
   __shared__ float red[8][MS * 16 * NREP];
   __shared__ float nss[NORM ? 8 : 1][MS];
@@ -1797,7 +1797,7 @@ __global__ __launch_bounds__(512) void gemm_gated_pipe_kernel(
   const int grp = blockIdx.x;               // 64-row group: 32 features
   // epilogue operands first: thread t owns row t / 16, features
   // grp * 32 + h * 16 + t % 16 (h = 0, 1)
-  const int pm = min((int)(threadIdx.x >> 4), M - 1);
+  const int pm = min((int)(threadIdx.x >> 4) & (MS - 1), M - 1);
   EpiGatedGelu::Pref pf[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -2956,12 +2956,19 @@ int cadence_gemm_linear_residual_rows(const void* A, int64_t lda, const void* W,
                 static_cast<const u16*>(resid), ld_resid, 0, RowMap{M, 0, 0}, 0.0f};
   epi.rows = static_cast<u16*>(out_rows);
   epi.mt = (int)((M + 15) / 16);
-  if (K == 2560 && M > 16 && lda == 0 && ldw == 0 && N % 16 == 0) {
-    // the output projection: unsplit, 16 waves per 16 columns
-    hipLaunchKernelGGL((gemm_resid_pipe_kernel<16, 5, 1, 5>), dim3((unsigned)(N / 16)),
-                       dim3(1024), 0, static_cast<hipStream_t>(stream),
-                       static_cast<const u16*>(A), static_cast<const u16*>(W), (int)M,
-                       (int)K, epi);
+  if (K == 2560 && lda == 0 && ldw == 0 && N % 16 == 0) {
+    // the output projection: unsplit, 16 waves per 16 columns (one or two
+    // 16-row tiles of packed rows)
+    if (M > 16)
+      hipLaunchKernelGGL((gemm_resid_pipe_kernel<16, 5, 1, 5, 2>), dim3((unsigned)(N / 16)),
+                         dim3(1024), 0, static_cast<hipStream_t>(stream),
+                         static_cast<const u16*>(A), static_cast<const u16*>(W), (int)M,
+                         (int)K, epi);
+    else
+      hipLaunchKernelGGL((gemm_resid_pipe_kernel<16, 5, 1, 5, 1>), dim3((unsigned)(N / 16)),
+                         dim3(1024), 0, static_cast<hipStream_t>(stream),
+                         static_cast<const u16*>(A), static_cast<const u16*>(W), (int)M,
+                         (int)K, epi);
     return (int)hipGetLastError();
   }
   launch_stream(static_cast<const u16*>(A), lda, static_cast<const u16*>(W), ldw, M, N,
@@ -2981,18 +2988,24 @@ int cadence_gemm_gated_gelu(const void* A, int64_t lda, const void* Wpacked,
   EpiGatedGelu epi{static_cast<u16*>(out), ldo,
                    static_cast<const u16*>(bias_gate),
                    static_cast<const u16*>(bias_up), (int)((M + 15) / 16)};
-  if (M > 16 && M <= 32 && ldw == 0 && lda == 0 && K % 32 == 0 && K <= 2560) {
-    // decode, 17..32 rows: the two-pair pipelined kernel (one round)
+  if (M <= 32 && ldw == 0 && lda == 0 && K % 32 == 0 && K <= 2560) {
+    // decode (packed rows, one or two 16-row tiles): the two-pair pipelined
+    // kernel (one round)
     const dim3 grid((unsigned)(F / 32));
     hipStream_t st = static_cast<hipStream_t>(stream);
     const u16* a = static_cast<const u16*>(A);
     const u16* w = static_cast<const u16*>(Wpacked);
-    if (norm)
-      hipLaunchKernelGGL((gemm_gated_pipe_kernel<10, 2, 3, true>), grid, dim3(512), 0, st, a,
-                         w, (int)M, (int)K, epi, norm_eps);
-    else
-      hipLaunchKernelGGL((gemm_gated_pipe_kernel<10, 2, 3, false>), grid, dim3(512), 0, st, a,
-                         w, (int)M, (int)K, epi, 0.0f);
+#define CADENCE_GP(NORM_, MR_, EPS_)                                                        \
+  hipLaunchKernelGGL((gemm_gated_pipe_kernel<10, 2, 3, NORM_, MR_>), grid, dim3(512), 0, st, a, \
+                     w, (int)M, (int)K, epi, EPS_)
+    if (M > 16) {
+      if (norm) CADENCE_GP(true, 2, norm_eps);
+      else CADENCE_GP(false, 2, 0.0f);
+    } else {
+      if (norm) CADENCE_GP(true, 1, norm_eps);
+      else CADENCE_GP(false, 1, 0.0f);
+    }
+#undef CADENCE_GP
     return (int)hipGetLastError();
   }
   return launch_gemm(static_cast<const u16*>(A), lda,

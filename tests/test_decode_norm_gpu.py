@@ -42,7 +42,8 @@ def _close(got, want, frac=0.25, tol=2e-2):
   assert eq >= frac, f"only {eq:.4f} bit-equal"
 
 
-@pytest.mark.parametrize("m,k", [(32, 2560), (32, 7680), (20, 2560), (1, 7680)])
+@pytest.mark.parametrize("m,k", [(32, 2560), (32, 7680), (20, 2560), (1, 7680), (5, 2560),
+                                 (1, 2560)])
 def test_residual_rows_match_two_kernel_path(dev, m, k):
   g = torch.Generator().manual_seed(41)
   n = 2560
@@ -55,9 +56,10 @@ def test_residual_rows_match_two_kernel_path(dev, m, k):
   out1, n1 = ops.linear_rmsnorm(a, w, bias, resid, norm)
   out2, r2 = ops.linear_rmsnorm(a, w, bias, resid, norm, lazy=True)
   assert isinstance(r2, ops.PackedRows) and r2.norm is norm
-  if k == 2560 and m > 16:
-    # the output projection's unsplit kernel (gemm_resid_pipe_kernel): one
-    # fp32 chain over all of K instead of the split-order sums
+  if k == 2560:
+    # the output projection's unsplit kernel (gemm_resid_pipe_kernel, one or
+    # two 16-row tiles): one fp32 chain over all of K instead of the
+    # split-order sums
     _close(out2, out1, frac=0.99)
   else:
     assert torch.equal(out1, out2)
@@ -152,11 +154,12 @@ def test_pending_norm_rows_materialise_for_other_consumers(dev):
   assert torch.equal(ops.linear(lazy, w), ops.linear(normed, w))
 
 
-@pytest.mark.parametrize("m", [32, 20])
+@pytest.mark.parametrize("m", [32, 20, 16, 7, 1])
 def test_gated_pipe_kernel_matches_stream_kernel(dev, m):
-  """The two-pair pipelined decode up-projection (packed rows, 17..32 rows)
-  sums in the one-pair stream kernel's order: bit-identical outputs at the
-  2B model's shape (F = 7680, K = 2560)."""
+  """The two-pair pipelined decode up-projection (packed rows: one 16-row
+  tile up to 16 rows -- the B = 1 decode of C3 -- two up to 32) sums in the
+  one-pair stream kernel's order: bit-identical outputs at the 2B model's
+  shape (F = 7680, K = 2560)."""
   g = torch.Generator().manual_seed(61)
   f, k = 7680, 2560
   x = rnd(m, k, gen=g).to(dev)
