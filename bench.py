@@ -90,6 +90,11 @@ def parse():
   ap.add_argument("--no-pipeline", action="store_true",
                   help="run the micro-batches back to back (generate per "
                   "micro-batch) instead of Sampler.generate_many's pipeline")
+  ap.add_argument("--no-continuous", action="store_true",
+                  help="lab A/B: join the pipeline lanes at the end of every "
+                  "step (no overlap of step i + 1's first prefill with step "
+                  "i's last decode; one micro-batch per rank then runs plain "
+                  "Sampler.generate)")
   ap.add_argument("--split-single", action="store_true",
                   help="lab: a rank whose share is one micro-batch runs it as "
                   "two pipelined halves (generate_many) instead of whole; "
@@ -356,6 +361,7 @@ def main():
   strong = bool(args.global_batch)
   gb = args.global_batch if strong else args.batch * world
   pipelined_plan = bool(args.decode and not args.no_pipeline and args.split_single)
+  continuous = not args.no_continuous
   lo, hi, micro = shard_plan(gb, args.batch, rank, world,
                              lanes=2 if pipelined_plan else 1)
   n_micro = len(micro)
@@ -369,7 +375,36 @@ def main():
   positions = torch.arange(args.prompt, dtype=torch.int32, device=dev)[None].repeat(
       mb, 1)
 
-  def step(events=None, pipeline=True):
+  gather_stream = torch.cuda.Stream()
+  # under a process group the continuous loop is issued from its own
+  # stream, not the null stream: an event on the legacy null stream waits
+  # for every blocking stream (RCCL's among them), which chains step i + 1's
+  # lanes to step i's all-gather (a rank's N = 8 load under an RCCL group of
+  # one: 111 ms per step from the null stream, 94 from its own stream,
+  # 104 without the continuous lanes; profiles/r04za_*).  Without a group
+  # the null stream measured faster (96-98 vs 109 ms).  The inputs are made
+  # before the timed loop.
+  issue_stream = (torch.cuda.Stream() if torch.distributed.is_available() and
+                  torch.distributed.is_initialized() else torch.cuda.current_stream())
+
+  def step(events=None, pipeline=True, done_event=None):
+    if args.decode and pipeline and not args.no_pipeline and continuous:
+      # a serving loop: micro-batches take the two lanes in turn across
+      # steps (Sampler.generate_many continuous), so micro-batch j + 1's
+      # prefill overlaps micro-batch j's decode also across a step boundary
+      # (at N = 8 a rank's one micro-batch per step overlaps the next
+      # step's); the step's rows are gathered on their own stream once both
+      # lanes have produced them.  `events` time the last micro-batch
+      with torch.cuda.stream(issue_stream):
+        sts = sampler.generate_many(
+            [(tokens[sl], lengths, None if images is None else images[sl])
+             for sl in micro], args.decode, events=events, continuous=True)
+      sampler.hand_over(sts, gather_stream)
+      with torch.cuda.stream(gather_stream):
+        out = D.gather_rows(torch.cat([st.tokens_buffer for st in sts]))
+        if done_event is not None:
+          done_event.record()
+      return out
     # (one micro-batch has nothing to overlap: plain Sampler.generate)
     if args.decode and pipeline and not args.no_pipeline and n_micro > 1:
       # micro-batch j + 1's prefill overlaps micro-batch j's decode
@@ -428,8 +463,9 @@ def main():
       # the kernel-timing pass runs the micro-batches one after another: with
       # two lanes in flight an event pair would also time the queueing behind
       # the other lane's kernels, not the launch itself
-      o = step(ev, pipeline=not kernel_timing)
-      sev[i + 1].record()
+      o = step(ev, pipeline=not kernel_timing, done_event=sev[i + 1])
+      if not (continuous and not kernel_timing and args.decode and not args.no_pipeline):
+        sev[i + 1].record()
       evs.append(ev)
     # host time to enqueue the K steps (no sync inside a step): under the
     # device time means the host runs ahead and the GPU does not wait on it
@@ -449,7 +485,7 @@ def main():
     dt, step_ev, ev_list, out = timed_pass(False)
     host_ms = host_enqueue["s"] * 1e3 / args.steps
     ksum = {}
-    pipelined = bool(args.decode and not args.no_pipeline and n_micro > 1)
+    pipelined = bool(args.decode and not args.no_pipeline and (n_micro > 1 or continuous))
     if not args.no_kernel_timing:
       _, _, ev_seq, _ = timed_pass(True)
       ksum = ops.TIMER.summary()
@@ -461,8 +497,12 @@ def main():
       if pipelined:
         ev_list = ev_seq
   elapsed = D.max_over_ranks(dt)
-  per_step = sorted(step_ev[i].elapsed_time(step_ev[i + 1])
-                    for i in range(args.steps))
+  # with the lanes carried across steps (continuous) consecutive steps
+  # finish alternately early and late: the median is taken over two-step
+  # windows (per step)
+  win = 2 if (continuous and args.decode and not args.no_pipeline and args.steps >= 2) else 1
+  per_step = sorted(step_ev[i].elapsed_time(step_ev[i + win]) / win
+                    for i in range(args.steps + 1 - win))
   median_ms = D.max_over_ranks(per_step[len(per_step) // 2])
   prefill_ms = []
   decode_ms = []
@@ -546,7 +586,9 @@ def main():
             "seq_len": n_vis + args.prompt + args.decode,
             "parallelism": f"dp{world}",
             "micro_batch_pipeline": bool(args.decode and not args.no_pipeline
-                                         and n_micro > 1),
+                                         and (n_micro > 1 or continuous)),
+            "pipeline_across_steps": bool(args.decode and not args.no_pipeline
+                                          and continuous),
         },
         "prefill_ms": round(pre_ms, 3),
         "prefill_timing": (("last micro-batch's prefill in the kernel-timing pass "
@@ -554,7 +596,8 @@ def main():
                             if not args.no_kernel_timing else
                             "last micro-batch's prefill, overlapping the previous "
                             "micro-batch's decode (Sampler.generate_many)")
-                           if args.decode and not args.no_pipeline and n_micro > 1
+                           if args.decode and not args.no_pipeline and
+                           (n_micro > 1 or continuous)
                            else "last micro-batch's prefill (headline pass)"),
         "prefill_tokens_per_s": round(prefill_tps, 1),
         "roofline": roofline_entry(ksum, dom, "mfma", args.config) if dom else None,

@@ -262,17 +262,25 @@ class Sampler:
 
   @torch.no_grad()
   def generate_many(self, batches: Sequence[tuple], total_generation_steps: int,
-                    lanes: int = 2, events: dict | None = None
-                    ) -> list[SamplingState]:
+                    lanes: int = 2, events: dict | None = None,
+                    continuous: bool = False) -> list[SamplingState]:
     """Generation for a sequence of micro-batches, pipelined over `lanes`
     streams: micro-batch j runs whole (prefill, then its decode graph
-    replays) on lane j % lanes, so one lane's prefill (MFMA-bound GEMMs, plus
-    the vision tower's side stream) overlaps another lane's decode steps (a
-    latency-bound GEMV chain) on the GPU.  Each lane has its own decode graph
-    (static buffers, arrival counters).  `batches`: (tokens [B, T],
-    input_lengths [B], images or None) per micro-batch; the outputs equal
-    `generate` on each in turn.  `events` applies to the last micro-batch.
-    Returns the states, ready on the caller's stream."""
+    replays) on one lane, the lanes taken in turn, so one lane's prefill
+    (MFMA-bound GEMMs, plus the vision tower's side stream) overlaps another
+    lane's decode steps (a latency-bound GEMV chain) on the GPU.  Each lane
+    has its own decode graph (static buffers, arrival counters).  `batches`:
+    (tokens [B, T], input_lengths [B], images or None) per micro-batch; the
+    outputs equal `generate` on each in turn.  `events` applies to the last
+    micro-batch.
+
+    Default: the lanes start after the caller's stream and the caller's
+    stream waits for them at return (the states are ready on it).
+    `continuous`: a serving loop's form -- the lanes wait only for the
+    caller's stream as it is at this call (the inputs), the turn of lanes
+    carries on from the previous continuous call, and nothing joins back:
+    the next call's first prefill overlaps this call's last decode.  Hand
+    the states to a consumer stream with `hand_over`."""
     dev = self.device
     cur = torch.cuda.current_stream(dev)
     ls = self.__dict__.setdefault("_lanes", {})
@@ -280,24 +288,56 @@ class Sampler:
     while len(streams) < lanes:
       streams.append(torch.cuda.Stream(device=dev))
     streams = streams[:lanes]
+    if continuous:
+      inputs = torch.cuda.Event()
+      inputs.record(cur)
+      first = self.__dict__.get("_lane_next", 0) % lanes
+    else:
+      first = 0
+    used = []
     for s in streams:
-      s.wait_stream(cur)
+      if continuous:
+        s.wait_event(inputs)
+      else:
+        s.wait_stream(cur)
     states = []
     for j, (tokens, lengths, images) in enumerate(batches):
       ev = events if j == len(batches) - 1 else None
-      with torch.cuda.stream(streams[j % lanes]):
+      lane = (first + j) % lanes
+      if lane not in used:
+        used.append(lane)
+      with torch.cuda.stream(streams[lane]):
         states.append(self.generate(tokens, lengths, total_generation_steps,
-                                    images=images, events=ev, slot=j % lanes))
+                                    images=images, events=ev, slot=lane))
+    if continuous:
+      self._lane_next = (first + len(batches)) % lanes
+      self._ready = []
+      for lane in used:
+        e = torch.cuda.Event()
+        e.record(streams[lane])
+        self._ready.append(e)
+      return states
     for s in streams:
       cur.wait_stream(s)
-    for st in states:   # allocated on a lane stream, handed to the caller's
+    self._record(states, cur)
+    return states
+
+  def hand_over(self, states: Sequence[SamplingState], stream) -> None:
+    """Makes `stream` wait for the lanes of the last continuous
+    `generate_many` and hands the states' memory to it."""
+    for e in getattr(self, "_ready", ()):
+      stream.wait_event(e)
+    self._record(states, stream)
+
+  @staticmethod
+  def _record(states, stream):
+    for st in states:   # allocated on a lane stream, used on `stream`
       for t in (st.tokens_buffer, st.step, st.positions, st.done):
-        if t.is_cuda:
-          t.record_stream(cur)
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+          t.record_stream(stream)
       for v in (st.cache or {}).values():
         for t in v:
-          t.record_stream(cur)
-    return states
+          t.record_stream(stream)
 
   def _sample(self, logits: torch.Tensor) -> torch.Tensor:
     if self.greedy_sampling:

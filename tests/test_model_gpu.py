@@ -310,6 +310,50 @@ def test_generate_many_pipeline_matches_sequential(dev):
           assert torch.equal(a, c), name
 
 
+def test_generate_many_continuous_across_calls(dev):
+  """generate_many(continuous=True), the bench's serving-loop form: the
+  lanes are taken in turn across calls (an odd micro-batch count, so the
+  second call starts on the other lane) and never joined back; after
+  hand_over to a consumer stream the tokens, positions and caches equal one
+  generate per micro-batch -- also for calls of a single micro-batch (a
+  rank's share at N = 8), whose consecutive calls overlap."""
+  cfg = small_config(window=64)
+  m, _ = make_model(dev, cfg, seed=51)
+  vocab = MockVocab()
+  g = torch.Generator().manual_seed(52)
+  b, t, steps = 4, 10, 7
+  calls = []
+  for n in (3, 1, 1, 2):
+    bs = []
+    for _ in range(n):
+      tok = torch.randint(3, cfg.vocab_size, (b, t), generator=g, dtype=torch.int32)
+      bs.append((tok.to(dev), torch.full((b,), t, dtype=torch.int32), None))
+    calls.append(bs)
+  seq = cadence.Sampler(m, vocab, use_graph=True)
+  want = [[seq.generate(tk, ln, steps) for tk, ln, _ in bs] for bs in calls]
+  pipe = cadence.Sampler(m, vocab, use_graph=True)
+  consumer = torch.cuda.Stream()
+  outs = []
+  for bs in calls:
+    got = pipe.generate_many(bs, steps, continuous=True)
+    pipe.hand_over(got, consumer)
+    with torch.cuda.stream(consumer):
+      outs.append([st.tokens_buffer.clone() for st in got])
+    outs[-1].append(got)
+  torch.cuda.synchronize()
+  for ws, os_ in zip(want, outs):
+    got = os_[-1]
+    for w, tb, gt in zip(ws, os_[:-1], got):
+      assert torch.equal(w.tokens_buffer.cpu(), tb.cpu())
+      assert torch.equal(w.positions.cpu(), gt.positions.cpu())
+      for name, cw in w.cache.items():
+        for a, c in zip(cw, gt.cache[name]):
+          if a.dim() == 4:
+            n = int(cw.num_tokens.max())
+            a, c = a[:, :n], c[:, :n]
+          assert torch.equal(a, c), name
+
+
 def test_decode_graph_counters_not_shared_after_stream_pool_wraps(dev):
   """A captured decode graph owns its split-combine arrival counters: once
   torch's stream pool (32 handles, round robin) hands the capture stream's
