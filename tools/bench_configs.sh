@@ -5,8 +5,10 @@
 # usage: tools/bench_configs.sh TAG
 tag=${1:?tag}
 S=tools/gpu_step.sh
+# (6 steps: the continuous lanes overlap step i + 1's prefill with step i's
+# decode from the second step on)
 for c in c2 c3 c4; do
-  $S 600 ${tag}_bench_$c.log python -u bench.py --config $c --steps 3 --warmup 1; rc=$?
+  $S 600 ${tag}_bench_$c.log python -u bench.py --config $c --steps 6 --warmup 1; rc=$?
   [ $rc = 99 ] && exit 1
   grep '^{' gpurun_out/${tag}_bench_$c.log > gpurun_out/${tag}_bench_$c.json || true
 done
