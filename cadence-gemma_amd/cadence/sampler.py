@@ -32,6 +32,8 @@ from __future__ import annotations
 import dataclasses
 from typing import Generic, NamedTuple, Sequence, TypeVar
 
+import os
+
 import torch
 
 from . import common, ops
@@ -61,8 +63,8 @@ class SamplerOutput(NamedTuple):
 def _to_device(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
   """A host tensor on `dev` without blocking the host (pinned staging; the
   caching host allocator keeps the block until the copy has run)."""
-  if dev.type != "cuda" or t.is_cuda:
-    return t.to(dev)
+  if dev.type != "cuda" or t.is_cuda or os.environ.get("CADENCE_SYNC_H2D") == "1":
+    return t.to(dev)        # (the env switch: lab A/B of the blocking copy)
   return t.pin_memory().to(dev, non_blocking=True)
 
 
@@ -301,14 +303,24 @@ class Sampler:
       else:
         s.wait_stream(cur)
     states = []
+    pace = self.__dict__.setdefault("_lane_prefill", {})
+    pacing = os.environ.get("CADENCE_LANE_PACE", "1") == "1"
     for j, (tokens, lengths, images) in enumerate(batches):
-      ev = events if j == len(batches) - 1 else None
       lane = (first + j) % lanes
+      # the host runs at most one micro-batch ahead per lane: before queueing
+      # on a lane it waits for that lane's previous prefill to have finished
+      # (the decode after it may still run), so the lanes' queues stay
+      # shallow and alternate prefill / decode on the device
+      prev = pace.get((dev, lane))
+      if pacing and prev is not None:
+        prev.synchronize()
+      ev = events if (j == len(batches) - 1 and events is not None) else {}
       if lane not in used:
         used.append(lane)
       with torch.cuda.stream(streams[lane]):
         states.append(self.generate(tokens, lengths, total_generation_steps,
                                     images=images, events=ev, slot=lane))
+      pace[(dev, lane)] = ev.get("prefill_end")
     if continuous:
       self._lane_next = (first + len(batches)) % lanes
       self._ready = []
