@@ -718,9 +718,13 @@ int cadence_rnn_scan(const void* x, int64_t ldx, const void* a, int64_t lda,
     else launch_scan_chunked<64>(p, c, st);
     return (int)hipGetLastError();
   }
-  // Otherwise two channels per lane, 16-step register ring, one-wave
-  // workgroups (4.7 TB/s at B=32, L=319/2048, E=2560 on MI355X).
-  launch_scan<2, 16>(p, st);
+  // Otherwise two channels per lane, an 8-step register ring (two chunks in
+  // flight), one-wave workgroups.  Graph-replayed at B = 32, E = 2560 with
+  // the y gate (tools/scan_ab.py, profiles/r04zj_scan_ab.log): L = 319
+  // 40.4 -> 36.2 us against the 16-step ring (5.8 TB/s), L = 2048 289.9 ->
+  // 282.1 us; one channel per lane and a 4-step ring are slower, 24 / 32-step
+  // rings were slower in round 3 (profiles/r03ai_*).  Bitwise identical.
+  launch_scan<2, 8>(p, st);
   return (int)hipGetLastError();
 }
 
