@@ -361,10 +361,15 @@ def main():
   strong = bool(args.global_batch)
   gb = args.global_batch if strong else args.batch * world
   pipelined_plan = bool(args.decode and not args.no_pipeline and args.split_single)
-  continuous = not args.no_continuous
   lo, hi, micro = shard_plan(gb, args.batch, rank, world,
                              lanes=2 if pipelined_plan else 1)
   n_micro = len(micro)
+  # the lanes carried across steps where a step is one micro-batch (C2, C3,
+  # a rank's share at N = 8: 107 -> 95 ms per step); with several
+  # micro-batches per step the lanes already overlap inside it (N = 1:
+  # neutral, 747 vs 746 ms) and a continuous headline pass skews the
+  # sequential pass's decode timing (profiles/r04zm_*)
+  continuous = not args.no_continuous and n_micro == 1
   mb = micro[0].stop - micro[0].start          # samples per micro-batch
   tok_cpu, img_cpu = make_inputs(gb, lo, hi, args.image_size, args.prompt,
                                  cfg.vocab_size, args.text_only)
