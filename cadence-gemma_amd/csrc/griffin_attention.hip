@@ -249,34 +249,58 @@ __global__ __launch_bounds__(GA_MAXW * 64) void griffin_attn_kernel(GAArgs a) {
     // inline asm with their own lgkmcnt wait: the compiler's builtin for
     // them is followed by a vmcnt(0) (it waits for the next tile's DMA).
     const int tq = c16 >> 2, tp = c16 & 3;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    // software-pipelined: the four reads of step s + 1 go out before step
+    // s's MFMAs, and a counted wait (LDS returns in order) retires only step
+    // s's -- one LDS latency per tile instead of one per two dim tiles
+    constexpr int NSTEP = 2 * (NDT / 2);    // (key half, dim-tile pair)
+    auto vaddr = [&](int step, uint32_t (&ad)[4]) {
+      const int kk = step / (NDT / 2), d0 = 2 * (step % (NDT / 2));
       const int r1 = 32 * kk + 4 * g + tq, r2 = r1 + 16;
       const uint32_t a1 = vlds + r1 * 512 + 8 * (tp & 1);
       const uint32_t a2 = vlds + r2 * 512 + 8 * (tp & 1);
       const int x1 = (r1 & 7) << 1, x2 = (r2 & 7) << 1;
+      const int ch0 = 2 * d0 + (tp >> 1), ch1 = ch0 + 2;
+      ad[0] = a1 + 16 * (ch0 ^ x1);
+      ad[1] = a2 + 16 * (ch0 ^ x2);
+      ad[2] = a1 + 16 * (ch1 ^ x1);
+      ad[3] = a2 + 16 * (ch1 ^ x2);
+    };
+    auto vissue = [&](int step, uint2 (&w)[4]) {
+      uint32_t ad[4];
+      vaddr(step, ad);
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %4\n"
+          "ds_read_b64_tr_b16 %1, %5\n"
+          "ds_read_b64_tr_b16 %2, %6\n"
+          "ds_read_b64_tr_b16 %3, %7"
+          : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
+          : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
+          : "memory");
+    };
+    uint2 wv[2][4];
+    vissue(0, wv[0]);
 #pragma unroll
-      for (int d0 = 0; d0 < NDT; d0 += 2) {
-        const int ch0 = 2 * d0 + (tp >> 1), ch1 = ch0 + 2;
-        // four reads and their wait in ONE statement: the compiler cannot
-        // schedule a use of an output (or reuse its registers) before the
-        // wait, which it does with one statement per read
-        uint2 w1[2], w2[2];
-        asm volatile(
-            "ds_read_b64_tr_b16 %0, %4\n"
-            "ds_read_b64_tr_b16 %1, %5\n"
-            "ds_read_b64_tr_b16 %2, %6\n"
-            "ds_read_b64_tr_b16 %3, %7\n"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(w1[0]), "=&v"(w2[0]), "=&v"(w1[1]), "=&v"(w2[1])
-            : "v"(a1 + 16 * (ch0 ^ x1)), "v"(a2 + 16 * (ch0 ^ x2)),
-              "v"(a1 + 16 * (ch1 ^ x1)), "v"(a2 + 16 * (ch1 ^ x2))
-            : "memory");
+    for (int step = 0; step < NSTEP; ++step) {
+      uint2 (&cur)[4] = wv[step & 1];
+      if (step + 1 < NSTEP) {
+        vissue(step + 1, wv[(step + 1) & 1]);
+        asm volatile("s_waitcnt lgkmcnt(4)"
+                     : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3])
+                     :
+                     : "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3])
+                     :
+                     : "memory");
+      }
+      const int kk = step / (NDT / 2), d0 = 2 * (step % (NDT / 2));
+      // cur[0] / cur[1]: dims of d0 (rows r1 / r2), cur[2] / cur[3]: d0 + 1
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(w1[u].x, w1[u].y, w2[u].x, w2[u].y));
-          o[d0 + u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[kk], o[d0 + u], 0, 0, 0);
-        }
+      for (int u = 0; u < 2; ++u) {
+        const bf16x8 vf = __builtin_bit_cast(
+            bf16x8, make_uint4(cur[2 * u].x, cur[2 * u].y, cur[2 * u + 1].x, cur[2 * u + 1].y));
+        o[d0 + u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[kk], o[d0 + u], 0, 0, 0);
       }
     }
     __syncthreads();   // this wave's DMA landed (vmcnt) + every wave done with buf
