@@ -1704,7 +1704,7 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
   }
 }
 
-// Decode residual projection of one K split (17..32 packed rows,
+// Decode residual projection of one K split (1..32 packed rows in MR = 1 or 2 16-row tiles,
 // fragment-packed W, K <= 16 waves x KSW x 32): the 13 MB output projection
 // (K = 2560).  One workgroup = 16 output columns over all of K, 16 waves
 // streaming their k-steps in chunks of CH with INF chunks of weight +
@@ -1774,7 +1774,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_resid_pipe_kernel(
   epi.apply_pf(m, col0 + (o & 15), v, 0, pf);
 }
 
-// Decode gated up-projection (17..32 packed rows, fragment-packed W, one K
+// Decode gated up-projection (1..32 packed rows in MR 16-row tiles, fragment-packed W, one K
 // split): TWO gate / up pairs -- 64 packed columns, 32 features -- per
 // workgroup, so F = 7680 takes 240 workgroups, one round on the CUs (the
 // one-pair stream kernel needs 480: two rounds, each paying the memory
