@@ -31,7 +31,7 @@ KEYS = {
         r"rglru_gates_stream_kernel<256>", 3 * 10208 * 2560 * 2 + 10 * 512 * 256 * 2,
         "x in + a, normalised x out (bf16) + packed gate weights"),
     "gemm_gated_pipe_kernel<10, 2, 3, true> (decode)": (
-        r"gemm_gated_pipe_kernel<10, 2, 3, true>", 79134720,
+        r"gemm_gated_pipe_kernel<10, 2, 3, true(, 2)?>", 79134720,
         "2F x K bf16 weights + activations + out"),
     "gemm_stream_kernel<32, 10, 2, EpiResidRows> (decode)": (
         r"gemm_stream_kernel<32, 10, 2, [^>]*EpiResidRows[^>]*>", 2560 * 7680 * 2,
