@@ -303,24 +303,14 @@ class Sampler:
       else:
         s.wait_stream(cur)
     states = []
-    pace = self.__dict__.setdefault("_lane_prefill", {})
-    pacing = os.environ.get("CADENCE_LANE_PACE", "1") == "1"
     for j, (tokens, lengths, images) in enumerate(batches):
       lane = (first + j) % lanes
-      # the host runs at most one micro-batch ahead per lane: before queueing
-      # on a lane it waits for that lane's previous prefill to have finished
-      # (the decode after it may still run), so the lanes' queues stay
-      # shallow and alternate prefill / decode on the device
-      prev = pace.get((dev, lane))
-      if pacing and prev is not None:
-        prev.synchronize()
-      ev = events if (j == len(batches) - 1 and events is not None) else {}
+      ev = events if j == len(batches) - 1 else None
       if lane not in used:
         used.append(lane)
       with torch.cuda.stream(streams[lane]):
         states.append(self.generate(tokens, lengths, total_generation_steps,
                                     images=images, events=ev, slot=lane))
-      pace[(dev, lane)] = ev.get("prefill_end")
     if continuous:
       self._lane_next = (first + len(batches)) % lanes
       self._ready = []
