@@ -6,6 +6,10 @@
 # usage: tools/pmc_traffic.sh TAG REGEX   -> gpurun_out/TAG/pmc_*.csv
 set -o pipefail
 export TMPDIR=/tmp
+# rocprofv3's PMC mode segfaults in the runtime (hipEventRecord /
+# device_synchronize) with the sampler's asynchronous pinned prompt copies;
+# the blocking copy changes no kernel (round 4)
+export CADENCE_SYNC_H2D=1
 tag=${1:?tag}; rx=${2:?regex}
 out=gpurun_out/$tag
 mkdir -p $out
