@@ -68,7 +68,7 @@ CONFIGS = {
 }
 
 
-def parse():
+def parse(argv=None):
   ap = argparse.ArgumentParser()
   ap.add_argument("--gpus", type=int, default=1)
   ap.add_argument("--steps", type=int, default=5)
@@ -103,13 +103,57 @@ def parse():
                   "whatever its row count, so two halves stream them twice)")
   ap.add_argument("--gemm-engine", type=int, default=None,
                   help="lab A/B: prefill GEMM engine plan (cadence_gemm_set_engine)")
-  args = ap.parse_args()
+  ap.add_argument("--serving-pass", action="store_true", default=None,
+                  help="after the headline pass, time K more steps with the "
+                  "lanes carried across steps (a serving loop: step i + 1's "
+                  "prefill overlaps step i's decode) and report them as "
+                  "value_serving; on by default for C3, whose value is the "
+                  "single-request rate")
+  ap.add_argument("--rehearsal", choices=["cpu"], default=None,
+                  help="no GPU: the launch / sharding / input generation / "
+                  "gather / max-over-ranks path of the bench over gloo with a "
+                  "deterministic per-sample digest standing in for the model "
+                  "(the CPU test of the self-spawned multi-rank path)")
+  args = ap.parse_args(argv)
   for k, v in CONFIGS[args.config].items():
     if getattr(args, k) is None:
       setattr(args, k, v)
   if args.cpu_decode_steps is None:
     args.cpu_decode_steps = args.decode
+  if args.serving_pass is None:
+    args.serving_pass = args.config == "c3"
   return args
+
+
+def launch_ranks(n: int, argv) -> int:
+  """`python bench.py --gpus N` outside a launcher: starts N rank processes
+  through torch.distributed.run on 127.0.0.1 (one per GPU: RANK / LOCAL_RANK
+  / WORLD_SIZE in their environment) and returns their exit code.  Called
+  before this process touches the GPU, and as a child process (never an
+  exec), so the launcher's ranks are the only processes that open a
+  device."""
+  import socket
+  import subprocess
+  s = socket.socket()
+  s.bind(("127.0.0.1", 0))
+  port = s.getsockname()[1]
+  s.close()
+  cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+         f"--nproc-per-node={n}", "--master-addr=127.0.0.1",
+         f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+  env = dict(os.environ)
+  env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this host
+  return subprocess.call(cmd, env=env)
+
+
+def prefill_rates(mb: int, tokens_per_sample: int, prefill_ms_max: float,
+                  world: int) -> tuple[float, float]:
+  """(aggregate, per-rank) prefill tokens/s: every rank prefills `mb` samples
+  of `tokens_per_sample` tokens in the timed micro-batch, and the slowest
+  rank's prefill time bounds the job (global prefill tokens / max-over-ranks
+  prefill time, SURVEY §8d: the >= 6x target is on the aggregate)."""
+  per_rank = mb * tokens_per_sample / (prefill_ms_max * 1e-3)
+  return per_rank * world, per_rank
 
 
 def build_model(dev, image_size, text_only):
@@ -346,11 +390,105 @@ def cpu_baseline(model, cfg, vis, tokens, images, decode_steps, budget_s=30.0):
           "samples": n, "seconds": round(dt, 2)}
 
 
-def main():
-  args = parse()
+def rehearsal_rows(tok, img, decode, vocab):
+  """Stand-in for one micro-batch's generated tokens in the CPU rehearsal: a
+  deterministic function of each sample's prompt and image only, so the
+  gathered rows of any sharding equal a one-rank run's."""
+  base = tok.long().sum(1)
+  if img is not None:
+    base = base + (img * 255).round().long().flatten(1).sum(1)
+  steps = torch.arange(decode, dtype=torch.int64)
+  return ((base[:, None] * 31 + steps[None] * 7919) % vocab).to(torch.int32)
+
+
+def rehearse(args):
+  """--rehearsal cpu: the bench's multi-rank plumbing without a GPU (gloo):
+  launch, shard_plan, make_inputs, the per-step gather, max-over-ranks timing
+  and rank 0's JSON line (n_gpus, checksum, aggregate prefill rate)."""
+  rank, world, _ = D.init_from_env(backend="gloo")
+  if world != args.gpus:
+    raise RuntimeError(f"--gpus {args.gpus} but the process group has {world} ranks")
+  vocab = 256000
+  gb = args.global_batch or args.batch * world
+  lo, hi, micro = shard_plan(gb, args.batch, rank, world)
+  tok, img = make_inputs(gb, lo, hi, args.image_size, args.prompt, vocab,
+                         args.text_only)
+  n_vis = 0 if args.text_only else (args.image_size // 14) ** 2
+  D.barrier()
+  t0 = time.perf_counter()
+  tp = 0.0
+  for _ in range(args.steps):
+    outs = []
+    for sl in micro:
+      t1 = time.perf_counter()
+      outs.append(rehearsal_rows(tok[sl], None if img is None else img[sl],
+                                 args.decode, vocab))
+      tp = time.perf_counter() - t1
+    out = D.gather_rows(torch.cat(outs))
+  D.barrier()
+  elapsed = D.max_over_ranks(time.perf_counter() - t0)
+  mb = micro[0].stop - micro[0].start
+  agg, per = prefill_rates(mb, n_vis + args.prompt, D.max_over_ranks(tp) * 1e3 + 1e-6,
+                           world)
+  if rank == 0:
+    print(json.dumps({
+        "metric": "rehearsal (CPU, no model): " + METRIC, "n_gpus": world,
+        "steps": args.steps, "value": round(gb * (n_vis + args.prompt + args.decode)
+                                            * args.steps / elapsed, 2),
+        "config": {"global_batch": gb, "micro_batch": mb,
+                   "micro_batches_per_gpu": len(micro),
+                   "parallelism": f"dp{world}"},
+        "prefill_tokens_per_s": round(agg, 1),
+        "prefill_tokens_per_s_per_rank": round(per, 1),
+        "generated_tokens_checksum": int(out.long().sum().item()),
+        "gathered_rows": int(out.shape[0])}), flush=True)
+  D.barrier()
+  D.shutdown()
+
+
+def fail_fast(exc: BaseException) -> None:
+  """SURVEY §5 fail-fast: a rank that raises reports it, tears its process
+  group down (bounded: a peer blocked in a collective cannot hold it) and
+  exits non-zero, so the launcher stops the other ranks."""
+  import threading
+  import traceback
+  rank = os.environ.get("RANK", "0")
+  print(f"bench: rank {rank} failed: {exc!r}", file=sys.stderr)
+  traceback.print_exc()
+  sys.stderr.flush()
+  sys.stdout.flush()
+  t = threading.Thread(target=D.shutdown, daemon=True)
+  t.start()
+  t.join(timeout=10)
+  os._exit(1)
+
+
+def main(argv=None):
+  args = parse(argv)
+  in_launcher = "WORLD_SIZE" in os.environ
+  if args.gpus > 1 and not in_launcher:
+    # before any GPU call: this process only launches the ranks
+    sys.exit(launch_ranks(args.gpus, sys.argv[1:] if argv is None else argv))
+  try:
+    if args.rehearsal:
+      rehearse(args)
+    else:
+      run(args)
+  except Exception as e:  # noqa: BLE001 -- every failure ends the job
+    fail_fast(e)
+
+
+def run(args):
   rank, world, local = D.init_from_env()
-  if world != args.gpus and rank == 0:
-    print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+  if world != args.gpus:
+    raise RuntimeError(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch with "
+                       f"torch.distributed.run --nproc-per-node {args.gpus}, or "
+                       f"run `python bench.py --gpus {args.gpus}` outside a "
+                       "launcher and it starts the ranks itself")
+  if torch.cuda.device_count() < world and os.environ.get(
+      "CADENCE_DIST_BACKEND") != "gloo":
+    raise RuntimeError(f"{world} ranks but {torch.cuda.device_count()} GPU(s) "
+                       "visible (RCCL needs one GPU per rank)")
   dev = torch.device("cuda", D.local_device_index(local))
   torch.cuda.set_device(dev)
   if args.gemm_engine is not None:
@@ -364,12 +502,15 @@ def main():
   lo, hi, micro = shard_plan(gb, args.batch, rank, world,
                              lanes=2 if pipelined_plan else 1)
   n_micro = len(micro)
-  # the lanes carried across steps where a step is one micro-batch (C2, C3,
-  # a rank's share at N = 8: 107 -> 95 ms per step); with several
+  # the lanes carried across steps where a step is one micro-batch (C2, a
+  # rank's share at N = 8: 107 -> 95 ms per step); with several
   # micro-batches per step the lanes already overlap inside it (N = 1:
   # neutral, 747 vs 746 ms) and a continuous headline pass skews the
-  # sequential pass's decode timing (profiles/r04zm_*)
-  continuous = not args.no_continuous and n_micro == 1
+  # sequential pass's decode timing (profiles/r04zm_*).  C3 is a latency
+  # config: its value is one request at a time, the two-requests-in-flight
+  # rate goes to value_serving (--serving-pass)
+  can_continue = bool(args.decode and not args.no_pipeline and n_micro == 1)
+  continuous = can_continue and not args.no_continuous and not args.serving_pass
   mb = micro[0].stop - micro[0].start          # samples per micro-batch
   tok_cpu, img_cpu = make_inputs(gb, lo, hi, args.image_size, args.prompt,
                                  cfg.vocab_size, args.text_only)
@@ -391,9 +532,14 @@ def main():
   # before the timed loop.
   issue_stream = (torch.cuda.Stream() if torch.distributed.is_available() and
                   torch.distributed.is_initialized() else torch.cuda.current_stream())
+  # the model's packing kernels and the input copies ran on the current
+  # stream: the issue stream starts after them whatever those copies were
+  issue_stream.wait_stream(torch.cuda.current_stream())
 
-  def step(events=None, pipeline=True, done_event=None):
-    if args.decode and pipeline and not args.no_pipeline and continuous:
+  def step(events=None, pipeline=True, done_event=None, lanes_across=None):
+    if lanes_across is None:
+      lanes_across = continuous
+    if pipeline and can_continue and lanes_across:
       # a serving loop: micro-batches take the two lanes in turn across
       # steps (Sampler.generate_many continuous), so micro-batch j + 1's
       # prefill overlaps micro-batch j's decode also across a step boundary
@@ -447,7 +593,7 @@ def main():
 
   host_enqueue = {}
 
-  def timed_pass(kernel_timing: bool):
+  def timed_pass(kernel_timing: bool, lanes_across=None):
     """K steps between barrier + synchronize; with kernel_timing a seeded
     1/4 of the prefill GEMM / attention / scan launches carry HIP events on
     their stream (ops.TIMER).  Returns (seconds, step events, per-step
@@ -468,8 +614,10 @@ def main():
       # the kernel-timing pass runs the micro-batches one after another: with
       # two lanes in flight an event pair would also time the queueing behind
       # the other lane's kernels, not the launch itself
-      o = step(ev, pipeline=not kernel_timing, done_event=sev[i + 1])
-      if not (continuous and not kernel_timing and args.decode and not args.no_pipeline):
+      across = continuous if lanes_across is None else lanes_across
+      o = step(ev, pipeline=not kernel_timing, done_event=sev[i + 1],
+               lanes_across=across)
+      if not (across and can_continue and not kernel_timing):
         sev[i + 1].record()
       evs.append(ev)
     # host time to enqueue the K steps (no sync inside a step): under the
@@ -482,7 +630,10 @@ def main():
     return t1 - t0, sev, evs, o
 
   with torch.no_grad():
-    for _ in range(args.warmup):
+    # the continuous lanes take one micro-batch per step in turn: each lane
+    # captures its decode graph on its first micro-batch, so the untimed
+    # warmup covers at least one step per lane
+    for _ in range(max(args.warmup, 2) if continuous else args.warmup):
       out = step()
     torch.cuda.synchronize()
     # the headline pass carries no per-kernel events (they cost the stream
@@ -501,14 +652,27 @@ def main():
       # events would inflate it)
       if pipelined:
         ev_list = ev_seq
+    serving = None
+    if args.serving_pass and can_continue:
+      # a serving loop over the same K steps: the lanes carried across steps,
+      # two requests in flight (one prefills while the other decodes)
+      # (at least one step per lane: each lane captures its decode graph on
+      # its first micro-batch, which must not fall in the timed steps)
+      for _ in range(max(args.warmup, 2)):
+        step(lanes_across=True)
+      torch.cuda.synchronize()
+      sdt, _, _, _ = timed_pass(False, lanes_across=True)
+      serving = D.max_over_ranks(sdt)
   elapsed = D.max_over_ranks(dt)
   # with the lanes carried across steps (continuous) consecutive steps
-  # finish alternately early and late: the median is taken over two-step
-  # windows (per step)
-  win = 2 if (continuous and args.decode and not args.no_pipeline and args.steps >= 2) else 1
+  # finish alternately early and late: the median is taken over
+  # non-overlapping two-step windows (per step)
+  win = 2 if (continuous and args.steps >= 2) else 1
   per_step = sorted(step_ev[i].elapsed_time(step_ev[i + win]) / win
-                    for i in range(args.steps + 1 - win))
-  median_ms = D.max_over_ranks(per_step[len(per_step) // 2])
+                    for i in range(0, args.steps + 1 - win, win))
+  mid = len(per_step) // 2
+  median_ms = D.max_over_ranks(per_step[mid] if len(per_step) % 2 else
+                               0.5 * (per_step[mid - 1] + per_step[mid]))
   prefill_ms = []
   decode_ms = []
   for ev in ev_list:
@@ -526,8 +690,8 @@ def main():
   ms_step = elapsed / args.steps * 1e3
   pre_ms = sum(prefill_ms) / max(len(prefill_ms), 1)
   pre_ms = D.max_over_ranks(pre_ms)
-  prefill_tps = mb * (n_vis + args.prompt - (1 if args.decode else 0)) / (
-      pre_ms * 1e-3)
+  prefill_tps, prefill_tps_rank = prefill_rates(
+      mb, n_vis + args.prompt - (1 if args.decode else 0), pre_ms, world)
 
   result = None
   if rank == 0:
@@ -592,8 +756,8 @@ def main():
             "parallelism": f"dp{world}",
             "micro_batch_pipeline": bool(args.decode and not args.no_pipeline
                                          and (n_micro > 1 or continuous)),
-            "pipeline_across_steps": bool(args.decode and not args.no_pipeline
-                                          and continuous),
+            "requests_in_flight": 2 if continuous else (1 if n_micro == 1 else n_micro),
+            "pipeline_across_steps": continuous,
         },
         "prefill_ms": round(pre_ms, 3),
         "prefill_timing": (("last micro-batch's prefill in the kernel-timing pass "
@@ -605,6 +769,10 @@ def main():
                            (n_micro > 1 or continuous)
                            else "last micro-batch's prefill (headline pass)"),
         "prefill_tokens_per_s": round(prefill_tps, 1),
+        "prefill_tokens_per_s_per_rank": round(prefill_tps_rank, 1),
+        "prefill_tokens_per_s_definition": (
+            "aggregate over ranks: world x micro-batch x prefill tokens per "
+            "sample / max-over-ranks prefill time of the timed micro-batch"),
         "roofline": roofline_entry(ksum, dom, "mfma", args.config) if dom else None,
         "roofline_scan": roofline_entry(ksum, scan_key, "hbm", args.config)
                          if scan_key else None,
@@ -635,6 +803,13 @@ def main():
                          "queueing behind the other lane)",
         "generated_tokens_checksum": int(out.long().sum().item()),
     }
+    if serving is not None:
+      result["value_serving"] = round(tok_per_step * args.steps / serving, 2)
+      result["ms_per_step_serving"] = round(serving / args.steps * 1e3, 3)
+      result["value_serving_definition"] = (
+          "the same K steps with the two lanes carried across steps (a serving "
+          "loop: step i + 1's request prefills while step i's decodes; two "
+          "requests in flight); value is one request at a time")
     if world == 1 and not args.no_cpu_baseline:
       result["cpu_baseline"] = cpu_baseline(model, cfg, vis, tok_cpu, img_cpu,
                                             args.cpu_decode_steps)

@@ -309,8 +309,11 @@ class Sampler:
       if lane not in used:
         used.append(lane)
       with torch.cuda.stream(streams[lane]):
+        # lanes own decode graphs 1..lanes: a plain generate() (slot 0, the
+        # caller's stream) right after a continuous call, whose lanes are
+        # still replaying, never shares a graph's static buffers with them
         states.append(self.generate(tokens, lengths, total_generation_steps,
-                                    images=images, events=ev, slot=lane))
+                                    images=images, events=ev, slot=1 + lane))
     if continuous:
       self._lane_next = (first + len(batches)) % lanes
       self._ready = []

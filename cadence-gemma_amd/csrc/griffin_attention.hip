@@ -265,29 +265,39 @@ __global__ __launch_bounds__(GA_MAXW * 64) void griffin_attn_kernel(GAArgs a) {
       ad[2] = a1 + 16 * (ch1 ^ x1);
       ad[3] = a2 + 16 * (ch1 ^ x2);
     };
-    auto vissue = [&](int step, uint2 (&w)[4]) {
+    // step s + 1's reads and step s's counted wait are ONE asm statement
+    // (outputs: the new registers; in/out: the pending ones), so no
+    // compiler-placed copy of a still-loading register can sit between them
+    uint2 wv[2][4];
+    {
       uint32_t ad[4];
-      vaddr(step, ad);
+      vaddr(0, ad);
       asm volatile(
           "ds_read_b64_tr_b16 %0, %4\n"
           "ds_read_b64_tr_b16 %1, %5\n"
           "ds_read_b64_tr_b16 %2, %6\n"
           "ds_read_b64_tr_b16 %3, %7"
-          : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
+          : "=&v"(wv[0][0]), "=&v"(wv[0][1]), "=&v"(wv[0][2]), "=&v"(wv[0][3])
           : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
           : "memory");
-    };
-    uint2 wv[2][4];
-    vissue(0, wv[0]);
+    }
 #pragma unroll
     for (int step = 0; step < NSTEP; ++step) {
       uint2 (&cur)[4] = wv[step & 1];
       if (step + 1 < NSTEP) {
-        vissue(step + 1, wv[(step + 1) & 1]);
-        asm volatile("s_waitcnt lgkmcnt(4)"
-                     : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3])
-                     :
-                     : "memory");
+        uint2 (&nx)[4] = wv[(step + 1) & 1];
+        uint32_t ad[4];
+        vaddr(step + 1, ad);
+        asm volatile(
+            "ds_read_b64_tr_b16 %0, %8\n"
+            "ds_read_b64_tr_b16 %1, %9\n"
+            "ds_read_b64_tr_b16 %2, %10\n"
+            "ds_read_b64_tr_b16 %3, %11\n"
+            "s_waitcnt lgkmcnt(4)"
+            : "=&v"(nx[0]), "=&v"(nx[1]), "=&v"(nx[2]), "=&v"(nx[3]),
+              "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3])
+            : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
+            : "memory");
       } else {
         asm volatile("s_waitcnt lgkmcnt(0)"
                      : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3])

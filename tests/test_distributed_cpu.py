@@ -153,7 +153,11 @@ def _sp_worker(rank, world, port, q):
   sl = slice(rank * lr, (rank + 1) * lr)
   y, h = D.sequence_parallel_rnn_scan(x[:, sl], a[:, sl], reset[:, sl],
                                       h0 if rank == 0 else None, scan=R.rnn_scan)
-  q.put((rank, y, h))
+  # plain lists, not tensors: a tensor put in the queue is shared through a
+  # file descriptor the exiting child may close before the parent reads it
+  # (ConnectionResetError); bf16 and fp32 values are exact as Python floats
+  q.put((rank, y.float().tolist(), h.tolist()))
+  D.barrier()
   D.shutdown()
 
 
@@ -175,10 +179,60 @@ def test_sequence_parallel_scan_gloo(world):
     assert p.exitcode == 0
   x, a, reset, h0 = _sp_inputs()
   y_ref, h_ref = R.rnn_scan(x, a, reset, h0)
-  y = torch.cat([r[1] for r in res], dim=1)
+  y = torch.cat([torch.tensor(r[1]).to(torch.bfloat16) for r in res], dim=1)
   assert (y == y_ref).float().mean().item() > 0.99
   torch.testing.assert_close(y.float(), y_ref.float(), rtol=1e-2, atol=1e-2)
-  torch.testing.assert_close(res[-1][2], h_ref, rtol=1e-5, atol=1e-5)
+  torch.testing.assert_close(torch.tensor(res[-1][2]), h_ref, rtol=1e-5, atol=1e-5)
+
+
+def _run_bench(*argv, timeout=300):
+  import json
+  import subprocess
+  import sys
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  env = {k: v for k, v in os.environ.items()
+         if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+  r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *argv],
+                     cwd=root, env=env, capture_output=True, text=True,
+                     timeout=timeout)
+  assert r.returncode == 0, r.stderr[-3000:]
+  lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+  assert len(lines) == 1, r.stdout
+  return json.loads(lines[0]), r
+
+
+def test_bench_self_spawn_world2_gloo():
+  """`python bench.py --gpus 2` outside a launcher starts the two ranks
+  itself (torch.distributed.run, before any GPU call); through bench's own
+  shard_plan / make_inputs / gather the JSON line reports n_gpus 2 and the
+  gathered rows' checksum equals the one-rank run's (the CPU rehearsal: a
+  per-sample digest stands in for the model)."""
+  args = ("--rehearsal", "cpu", "--global-batch", "8", "--batch", "2",
+          "--image-size", "28", "--prompt", "6", "--decode", "3",
+          "--steps", "2", "--warmup", "0")
+  one, _ = _run_bench("--gpus", "1", *args)
+  two, _ = _run_bench("--gpus", "2", *args)
+  assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+  assert two["config"]["parallelism"] == "dp2"
+  assert two["gathered_rows"] == one["gathered_rows"] == 8
+  assert two["config"]["micro_batches_per_gpu"] == 2
+  assert two["generated_tokens_checksum"] == one["generated_tokens_checksum"]
+
+
+def test_bench_rank_failure_exits_nonzero():
+  """Fail-fast: a rank that raises (here: a global batch the ranks cannot
+  split) tears its group down and the launcher exits non-zero."""
+  import subprocess
+  import sys
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  env = {k: v for k, v in os.environ.items()
+         if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+  r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                      "--rehearsal", "cpu", "--global-batch", "6", "--batch", "2",
+                      "--image-size", "28", "--prompt", "6", "--decode", "3"],
+                     cwd=root, env=env, capture_output=True, text=True, timeout=300)
+  assert r.returncode != 0
+  assert "failed" in r.stderr
 
 
 def test_sp_carry_algebra_single_process():

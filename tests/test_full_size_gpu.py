@@ -69,6 +69,14 @@ MAX_ABS = 0.25
 COS = 0.999
 ACC = 1.25
 MARGIN = 0.2
+# every fixture row's sampler continuation is compared for at least this
+# many steps (the fixture seeds are chosen so the oracle's first decode steps
+# are margin-decided: tests/golden/seed_search.py)
+MIN_STEPS_COMPARED = 3
+# per-row reports (cosine, max-abs, rel-L2 vs fp32, steps compared) land
+# here on every run, pass or fail, for the evidence under profiles/
+REPORT_DIR = os.environ.get("CADENCE_PARITY_REPORT_DIR", os.path.join(
+    os.path.dirname(HERE), "gpurun_out", "parity"))
 
 
 class _Vocab:
@@ -229,8 +237,21 @@ def test_full_size_parity(dev, name):
       tok, torch.full((b,), t, dtype=torch.int32), steps, images=px)
   got = st.tokens_buffer.cpu()
   for i in range(b):
+    n = _check_tokens(got[i], f, i, f"{name} row {i}", bad)
+    if n < MIN_STEPS_COMPARED:
+      bad.append(f"{name} row {i}: sampler tokens compared for {n} steps "
+                 f"(floor {MIN_STEPS_COMPARED})")
     report[f"sampler[{i}]"] = {
-        "steps_compared": _check_tokens(got[i], f, i, f"{name} row {i}", bad),
+        "steps_compared": n, "tokens": got[i].tolist(),
+        "oracle_tokens": f["greedy_tokens"][i].tolist(),
         "distinct_oracle_tokens": len(set(f["greedy_tokens"][i].tolist()))}
+  report["argmax_enforced_rows"] = sum(
+      float(f["logit_margin"][i, j]) > _margin_bar(f, i, j)
+      for i in range(b) for j in range(1 + steps))
+  report["rows"] = b * (1 + steps)
+  report["violations"] = bad
   print(name, json.dumps(report), flush=True)
+  os.makedirs(REPORT_DIR, exist_ok=True)
+  with open(os.path.join(REPORT_DIR, f"full_{name}.json"), "w") as fh:
+    json.dump(report, fh, indent=1)
   assert not bad, "\n".join(bad)

@@ -354,6 +354,35 @@ def test_generate_many_continuous_across_calls(dev):
           assert torch.equal(a, c), name
 
 
+def test_generate_after_continuous_same_sampler(dev):
+  """A plain generate() on the caller's stream right after a continuous
+  generate_many on the SAME sampler, while the lanes may still replay their
+  decode graphs: the lanes own graph slots 1..lanes, generate() slot 0, so
+  no static buffer is shared and every output equals a fresh sampler's."""
+  cfg = small_config(window=64)
+  m, _ = make_model(dev, cfg, seed=61)
+  vocab = MockVocab()
+  g = torch.Generator().manual_seed(62)
+  b, t, steps = 4, 10, 12
+  mk = lambda: (torch.randint(3, cfg.vocab_size, (b, t), generator=g,
+                              dtype=torch.int32).to(dev),
+                torch.full((b,), t, dtype=torch.int32), None)
+  lane_in = [mk(), mk()]
+  plain_in = mk()
+  ref = cadence.Sampler(m, vocab, use_graph=True)
+  want_lanes = [ref.generate(tk, ln, steps) for tk, ln, _ in lane_in]
+  want_plain = ref.generate(plain_in[0], plain_in[1], steps)
+  s = cadence.Sampler(m, vocab, use_graph=True)
+  for _ in range(2):
+    got = s.generate_many(lane_in, steps, continuous=True)
+    plain = s.generate(plain_in[0], plain_in[1], steps)   # caller's stream
+    s.hand_over(got, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(plain.tokens_buffer.cpu(), want_plain.tokens_buffer.cpu())
+    for w, gt in zip(want_lanes, got):
+      assert torch.equal(w.tokens_buffer.cpu(), gt.tokens_buffer.cpu())
+
+
 def test_decode_graph_counters_not_shared_after_stream_pool_wraps(dev):
   """A captured decode graph owns its split-combine arrival counters: once
   torch's stream pool (32 handles, round robin) hands the capture stream's
