@@ -314,6 +314,42 @@ def vit_attention_isolated(vis, batch, dev, reps=20):
   return out
 
 
+def scan_isolated(batch, length, width, dev, reps=20):
+  """rnn_scan alone at the workload's recurrent shape (x, a, the y gate in;
+  y out; fp32 state out), HIP events around `reps` launches after the timed
+  region: the prefill path now runs the scan inside the fused gates + scan
+  kernel (rglru_scan_fused_kernel, VALU-bound by the gate chain), so the
+  scan kernel's own HBM fraction -- the north star's RG-LRU scan bar -- is
+  measured here; the same kernel runs where the fused plan does not apply
+  (C3, small batches) and behind the public rnn_scan API."""
+  g = torch.Generator(device=dev).manual_seed(5)
+  m = batch * length
+  x = torch.randn(m, width, device=dev, generator=g).to(torch.bfloat16)
+  a = torch.rand(m, width, device=dev, generator=g).to(torch.bfloat16)
+  gate = torch.randn(m, width, device=dev, generator=g).to(torch.bfloat16)
+  run = lambda: ops.ops.rnn_scan(x, a, None, None, gate, batch, length)
+  run()
+  torch.cuda.synchronize()
+  s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+  s.record()
+  for _ in range(reps):
+    run()
+  e.record()
+  torch.cuda.synchronize()
+  us = s.elapsed_time(e) / reps * 1e3
+  nbytes = m * width * 8 + batch * width * 4
+  from cadence import _lib
+  chunked = _lib.load().cadence_rnn_scan_workspace_bytes(batch, length, width) > 0
+  gbs = nbytes / (us * 1e-6) / 1e9
+  return {"kernel": "rnn_scan_chunk_kernel" if chunked else "rnn_scan_kernel",
+          "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+          "avg_us": round(us, 2), "work_per_launch": nbytes,
+          "shape": f"B={batch} L={length} E={width}",
+          "timing": f"isolated, {reps} launches after the timed region; 8 B per "
+                    "element (x, a, y gate in, y out, bf16) + fp32 state out"}
+
+
 def image_preprocess_isolated(batch, size, dev, reps=20, h=480, w=640):
   """img_path preprocessing (Resize((S,S), BICUBIC) + ToTensor, Pillow-exact)
   on `batch` synthetic h x w RGB uint8 images already resident in HBM, HIP
@@ -684,6 +720,11 @@ def run(args):
              if vis is not None and rank == 0 and not args.no_kernel_timing else None)
   img_iso = (image_preprocess_isolated(args.batch, args.image_size, dev)
              if vis is not None and rank == 0 and not args.no_kernel_timing else None)
+  scan_iso = None
+  if (rank == 0 and not args.no_kernel_timing and not any(
+      k in ksum for k in ("rnn_scan_kernel", "rnn_scan_chunk_kernel"))):
+    scan_iso = scan_isolated(mb, n_vis + args.prompt - (1 if args.decode else 0),
+                             cfg.lru_width, dev)
 
   tok_per_step = gb * (n_vis + args.prompt + args.decode)
   value = tok_per_step * args.steps / elapsed
@@ -774,8 +815,14 @@ def run(args):
             "aggregate over ranks: world x micro-batch x prefill tokens per "
             "sample / max-over-ranks prefill time of the timed micro-batch"),
         "roofline": roofline_entry(ksum, dom, "mfma", args.config) if dom else None,
-        "roofline_scan": roofline_entry(ksum, scan_key, "hbm", args.config)
-                         if scan_key else None,
+        "roofline_scan": (roofline_entry(ksum, scan_key, "hbm", args.config)
+                          if scan_key else scan_iso),
+        # prefill RG-LRU gates + scan fused (one launch per recurrent block):
+        # HBM-priced on x and the y gate in, y out, weights and state; the
+        # gate chain's VALU, not the bytes, bounds it
+        "roofline_rglru_fused": next((roofline_entry(ksum, k, "hbm", args.config)
+                                      for k in sorted(ksum)
+                                      if k.startswith("rglru_scan_fused_kernel")), None),
         "roofline_decode": dec,
         # prefill RG-LRU gates: HBM-priced (x in, a and normalised x out)
         "roofline_rglru_gates": next((roofline_entry(ksum, k, "hbm", args.config)

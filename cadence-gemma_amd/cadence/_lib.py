@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # CADENCE_LIB_PATH: the host-ASan build of the same C-ABI
 # (tools/asan_host.sh, CPU-only contract tests); unset everywhere else
 LIB_PATH = os.environ.get("CADENCE_LIB_PATH") or os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -43,6 +43,9 @@ _SIGS: dict[str, list] = {
     "cadence_rglru_gates": [P, I64, P, I64, P, P, P, P, P, P, I64, I64, I64, I64,
                             P, I64, P],
     "cadence_rglru_gates_stream_plan": [P, I64, P, I64, I64, I64, I64],
+    "cadence_rglru_scan": [P, I64, P, P, P, P, P, P, P, I64, P, I64, P, I64, I64,
+                           I64, I64, P],
+    "cadence_rglru_scan_plan": [P, I64, P, I64, I64, I64, I64, I64, I64],
     "cadence_gemm_rmsnorm_workspace_bytes": [I64, I64, I64],
     "cadence_qkv_rope_decode": [P, I64, P, I64, P, P, P, P, I64, I64, I64, I64, P,
                                 I64, I32, F32, P],

@@ -214,6 +214,19 @@ class RGLRU(nn.Module):
     w, bx, ba, sp = self.packed()
     return ops.rglru_gates(x2d, w, bx, ba, sp, pos_flat)
 
+  def gates_scan(self, x2d: torch.Tensor, pos_flat: torch.Tensor, h0, gate,
+                 b: int, t: int):
+    """Prefill: gates then rnn_scan (a with resets zeroed, so no positions)
+    joined with `gate` -> (bf16(h) [* gate] [B*T, E], h_last [B, E]); one
+    fused launch where the kernel's plan takes the shape (enough sequences x
+    blocks to fill the chip), the two kernels otherwise."""
+    w, bx, ba, sp = self.packed()
+    h, two_bw, bw = w.shape
+    if ops.rglru_scan_plan(x2d, gate, b, t, h, bw):
+      return ops.ops.rglru_scan(x2d, w, bx, ba, sp, pos_flat, h0, gate, b, t)
+    a, nx = ops.rglru_gates(x2d, w, bx, ba, sp, pos_flat)
+    return ops.ops.rnn_scan(nx, a, None, h0, gate, b, t)
+
   def step_(self, x2d: torch.Tensor, pos_flat: torch.Tensor, h: torch.Tensor,
             gate: torch.Tensor | None = None, packed_out: bool = False):
     """One token per row (T = 1): gates + scan step fused, `h` updated in

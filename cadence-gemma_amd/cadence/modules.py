@@ -264,10 +264,9 @@ class RecurrentBlock(nn.Module):
     y_br, x_br = yx[:, :e], yx[:, e:]
     conv_out, conv_state = self.conv_1d.apply2d(
         x_br, pos, None if cache is None else cache.conv1d_state, b, t)
-    a, nx = self.rg_lru.gates(conv_out, pos.view(-1))
     h0 = None if cache is None else cache.rg_lru_state
-    with trace("rnn_scan"):
-      gated, h_last = ops.ops.rnn_scan(nx, a, None, h0, y_br, b, t)
+    with trace("rg_lru"):
+      gated, h_last = self.rg_lru.gates_scan(conv_out, pos.view(-1), h0, y_br, b, t)
     out, hn = _out_proj(gated, self.linear_out, resid2d, norm)
     if not return_cache:
       return out, hn, None

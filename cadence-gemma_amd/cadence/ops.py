@@ -583,6 +583,44 @@ def _rglru_gates(x, w_packed, bias_x, bias_a, softplus_a, segment_pos,
   return a, nx
 
 
+def rglru_scan_plan(x, gate, B, L, heads, bw) -> bool:
+  """Host-only query: the fused gates + scan kernel takes these operands."""
+  return bool(_lib.load().cadence_rglru_scan_plan(
+      _p(x), x.stride(0), _p(gate), gate.stride(0) if gate is not None else 0,
+      heads * bw, B, L, heads, bw))
+
+
+@_reg("rglru_scan(Tensor x, Tensor w_packed, Tensor bias_x, Tensor bias_a, "
+      "Tensor softplus_a, Tensor segment_pos, Tensor? h0, Tensor? gate, int B, "
+      "int L) -> (Tensor, Tensor)")
+def _rglru_scan(x, w_packed, bias_x, bias_a, softplus_a, segment_pos, h0, gate,
+                B, L):
+  """Prefill gates + scan in one launch (rglru_gates then rnn_scan, bitwise):
+  returns (bf16(h) [* gate] [B * L, E], h_last [B, E] fp32)."""
+  ldx = _mat(x, "x")
+  M, E = x.shape
+  H, two_bw, bw = w_packed.shape
+  _need(two_bw == 2 * bw and H * bw == E and M == B * L, "w_packed / x shape")
+  _need(segment_pos.dtype == _I32 and segment_pos.numel() == M, "segment_pos")
+  ldg = _mat(gate, "gate") if gate is not None else 0
+  if h0 is not None:
+    _need(h0.dtype == _F32 and h0.is_contiguous() and tuple(h0.shape) == (B, E),
+          "h0: [B, E] fp32")
+  out = torch.empty(M, E, dtype=_BF16, device=x.device)
+  h_last = torch.empty(B, E, dtype=_F32, device=x.device)
+  ev = TIMER.start(x)
+  _lib.check(_lib.load().cadence_rglru_scan(
+      _p(x), ldx, _p(w_packed), _p(bias_x), _p(bias_a), _p(softplus_a),
+      _p(segment_pos.contiguous()), _p(h0), _p(gate), ldg, _p(out), E,
+      _p(h_last), B, L, H, bw, _s(x)), "rglru_scan")
+  # algorithmic HBM bytes: x (+ gate) in, y out (bf16 per element), the
+  # packed gate weights once, fp32 state out (+ in), int32 positions
+  nbytes = (M * E * (4 + (2 if gate is not None else 0)) + w_packed.numel() * 2
+            + B * E * 4 * (2 if h0 is not None else 1) + M * 4)
+  TIMER.stop(ev, f"rglru_scan_fused_kernel<{bw}>", nbytes, x)
+  return out, h_last
+
+
 @_reg("rglru_step_(Tensor x, Tensor w_packed, Tensor bias_x, Tensor bias_a, "
       "Tensor softplus_a, Tensor segment_pos, Tensor(a!) h, Tensor? gate, "
       "bool decode_layout=False, bool out_packed=False) -> Tensor")

@@ -547,9 +547,11 @@ struct EpiRglruGates {
                          bool reset, float& av, float& nx) const {
     const float gx = rbf(hw_sigmoid(gx_pre));
     const float ga = rbf(hw_sigmoid(ga_pre));
-    const float log_a = bmul(rbf(-8.0f * ga), sp);
+    // -8 ga and 2 log_a scale a bf16 value by a power of two: exact in bf16,
+    // so the reference's rounding of them is the identity (not re-done here)
+    const float log_a = bmul(-8.0f * ga, sp);
     const float a = rbf(hw_exp(log_a));
-    const float a_sq = rbf(hw_exp(rbf(2.0f * log_a)));
+    const float a_sq = rbf(hw_exp(2.0f * log_a));
     const float gated = bmul(xv, gx);
     const float mult = reset ? 1.0f : rbf(hw_sqrt(rbf(1.0f - a_sq)));
     av = reset ? 0.0f : a;
@@ -562,9 +564,9 @@ struct EpiRglruGates {
                           f32x2& av, f32x2& nx) const {
     const f32x2 gx = rbf2(f32x2{hw_sigmoid(gx_pre.x), hw_sigmoid(gx_pre.y)});
     const f32x2 ga = rbf2(f32x2{hw_sigmoid(ga_pre.x), hw_sigmoid(ga_pre.y)});
-    const f32x2 log_a = bmul2(rbf2(f32x2{-8.0f * ga.x, -8.0f * ga.y}), sp);
+    const f32x2 log_a = bmul2(f32x2{-8.0f * ga.x, -8.0f * ga.y}, sp);   // exact scalings
     const f32x2 a = rbf2(f32x2{hw_exp(log_a.x), hw_exp(log_a.y)});
-    const f32x2 l2 = rbf2(f32x2{2.0f * log_a.x, 2.0f * log_a.y});
+    const f32x2 l2 = f32x2{2.0f * log_a.x, 2.0f * log_a.y};
     const f32x2 a_sq = rbf2(f32x2{hw_exp(l2.x), hw_exp(l2.y)});
     const f32x2 gated = bmul2(xv, gx);
     const f32x2 om = rbf2(f32x2{sub_rn(1.0f, a_sq.x), sub_rn(1.0f, a_sq.y)});
@@ -2032,6 +2034,229 @@ __global__ __launch_bounds__(BW * 2) void rglru_gates_stream_kernel(
   }
 }
 
+// Prefill RG-LRU with the scan fused in (layers.py:321-375: both
+// BlockDiagonalLinear GEMMs, the gate chain, then rnn_scan :145-199 and the
+// `x * y` join of modules.py:652): the (a, normalised x) pair never goes to
+// HBM.  A workgroup owns one sequence b and 128 channels of one head block g
+// (4 waves x 32 channels) for the whole sequence, and walks it in chunks of
+// 32 time steps: the chunk's X rows (the block's BW conv outputs) and y-gate
+// rows are register-staged one chunk ahead into double LDS buffers; each
+// wave runs rglru_gates_stream_kernel's MFMAs (same fragments, same k order)
+// and chain2 for its 32 channels, parks the bf16 (a, nx) pairs in its own
+// LDS slab, and its lanes 0..31 then scan the chunk's 32 steps, one channel
+// per lane, in rnn_scan_kernel's op order (h = a h + nx in fp32, y =
+// bf16(h) [* gate]); the chunk's outputs leave as 16-B row segments.  Every
+// value and rounding point is the two-kernel path's: bitwise equal to
+// rglru_gates_stream_kernel + rnn_scan_kernel.  HBM traffic: x and the gate
+// in, y out (6 B per element) instead of 14; the gate chain's VALU (7
+// transcendentals, 14 bf16 rounding points per element) bounds it.
+// Workgroup n: unit (n / 16) * 8 + n % 8, half (n / 8) % 2 -- the two
+// halves of a (sequence, block) unit sit on one XCD (blocks n and n + 8) and
+// share its X rows through that XCD's L2.
+// LDS-DMA of 16 B per lane into M0 + 16 * lane, hidden from hipcc's waitcnt
+// pass (cdna_hip_programming.md §5.7: M0 is written and restored in the same
+// statement); the caller retires it with its own vmcnt wait + barrier.
+CADENCE_DEV void glds16_asm(const void* gsrc, uint32_t lds_byte) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_byte) : "memory");
+}
+CADENCE_DEV uint32_t lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)(p));
+}
+
+constexpr int kRglruScanMaxL = 4096;   // reset flags held in LDS
+
+struct RglruScanArgs {
+  const u16* x; int64_t ldx;          // conv output rows [B * L][E]
+  const u16* w;                       // packed gate weights [H][2 BW][BW]
+  const u16* bias_x; const u16* bias_a; const u16* softplus_a;
+  const int32_t* segpos;              // [B * L]
+  const float* h0;                    // [B][E] fp32 or null
+  const u16* gate; int64_t ldg;       // linear_y branch rows or null
+  u16* out; int64_t ldo;
+  float* h_last;                      // [B][E] fp32 or null
+  int B, L, E, H;
+};
+
+template <int BW, bool GATE, int RT>
+__global__ __launch_bounds__(256, 2) void rglru_scan_fused_kernel(RglruScanArgs p) {
+  constexpr int KS = BW / 32, CPR = BW / 8, RF = RT / 16;
+  constexpr int SWM = CPR >= 16 ? 15 : CPR - 1;
+  constexpr int NQ = BW / 128;                    // workgroups per block row
+  constexpr int AS = 33;                          // (a, nx) slab row stride (u32)
+  constexpr int NB = 3;                           // chunk buffers: DMA two chunks ahead
+  __shared__ uint4 xs[NB][RT * CPR];              // X rows of a chunk (swizzled)
+  __shared__ uint4 ys[NB][RT * 16];               // y-gate rows, this WG's 128 channels
+  __shared__ uint32_t an[4][RT * AS];             // per wave: bf16 a | nx << 16
+  __shared__ uint4 ob[4][RT * 4];                 // per wave: RT rows x 32 bf16 outputs
+  __shared__ uint8_t rs_[kRglruScanMaxL];         // reset flag of every step
+  const int n = blockIdx.x;
+  const int unit = (n >> 4) * 8 + (n & 7), q = (n >> 3) & 1;
+  if (unit >= p.B * p.H || q >= NQ) return;       // grid padding (workgroup-uniform)
+  const int b = unit / p.H, g = unit % p.H;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wih = 4 * q + wave;                   // wave's 32-channel group in the block
+  const int L = p.L;
+  const int64_t row0 = (int64_t)b * L;
+  const u16* X = p.x + (int64_t)g * BW;
+  const u16* wg = p.w + (int64_t)g * 2 * BW * BW;
+  const int nch = (L + RT - 1) / RT;
+  // chunk c's X / y-gate rows go HBM -> LDS by LDS-DMA (one wave instruction
+  // = 1 KiB of lane-linear LDS), rows clamped into the sequence (branch-free:
+  // every wave issues the same NDMA pieces per chunk, which the counted waits
+  // below rely on), issued by inline asm: hipcc would otherwise treat every
+  // later ds_read as possibly aliasing the DMA and wait vmcnt(0) in front of
+  // it.  The XOR chunk swizzle is applied to the per-lane source address (an
+  // involution: the fragment reads apply it again).  Wave w moves X pieces
+  // w, w + 4, ... and y pieces RF w .. RF w + RF - 1 (4 rows each).
+  constexpr int XRP = 1024 / (CPR * 16);          // X rows per 1 KiB piece
+  constexpr int XPC = RT / XRP;                   // X pieces per chunk
+  constexpr int NDMA = XPC / 4 + (GATE ? RF : 0); // DMA instructions per wave per chunk
+  static_assert(XPC % 4 == 0, "X pieces per wave");
+  const uint32_t xs0 = lds_addr(&xs[0][0]), ys0 = lds_addr(&ys[0][0]);
+  auto dma = [&](int c, int bfd) {
+    c = min(c, nch - 1);
+#pragma unroll
+    for (int i = 0; i < XPC / 4; ++i) {
+      const int pc = wave + 4 * i;
+      const int r = pc * XRP + lane / CPR, slot = lane % CPR;
+      const int t = min(c * RT + r, L - 1);
+      glds16_asm(X + (row0 + t) * p.ldx + 8 * (slot ^ (r & SWM)),
+                 xs0 + (uint32_t)(bfd * RT * CPR + pc * 64) * 16);
+    }
+    if constexpr (GATE) {
+#pragma unroll
+      for (int i = 0; i < RF; ++i) {
+        const int pc = RF * wave + i;
+        const int r = pc * 4 + lane / 16;
+        const int t = min(c * RT + r, L - 1);
+        glds16_asm(p.gate + (row0 + t) * p.ldg + g * BW + 128 * q + 8 * (lane % 16),
+                   ys0 + (uint32_t)(bfd * RT * 16 + pc * 64) * 16);
+      }
+    }
+  };
+  // the first two chunks' DMA flies under the weight loads and the flags
+  dma(0, 0);
+  dma(1, 1);
+  uint4 wf[4][KS];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      wf[j][ks] = ld16(wg + (int64_t)(64 * wih + 16 * j + (lane & 15)) * BW + ks * 32 +
+                       8 * (lane >> 4));
+  // reset flags of the whole sequence (positions read once, coalesced)
+  for (int t = threadIdx.x; t < L; t += 256) rs_[t] = p.segpos[row0 + t] == 0;
+  const int ch0 = 32 * wih + (lane & 15);         // channel in the block
+  const int e0 = g * BW + ch0;
+  const f32x2 bx{bf2f(p.bias_x[e0]), bf2f(p.bias_x[e0 + 16])};
+  const f32x2 ba{bf2f(p.bias_a[e0]), bf2f(p.bias_a[e0 + 16])};
+  const f32x2 sp{bf2f(p.softplus_a[e0]), bf2f(p.softplus_a[e0 + 16])};
+  float h = 0.0f;
+  const int es = g * BW + 32 * wih + (lane & 31);  // the channel this lane scans
+  if (p.h0) h = p.h0[(int64_t)b * p.E + es];
+  // every register load above has landed before the loop (one use of each
+  // weight register: rglru_gates_stream_kernel's note), so the only vector
+  // memory operations the loop waits for are its own, counted below
+  {
+    uint32_t chk = __float_as_uint(h) ^ __float_as_uint(bx.x + ba.y + sp.x);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) chk ^= wf[j][ks].x ^ wf[j][ks].y ^ wf[j][ks].z ^ wf[j][ks].w;
+    if (chk == 0x6b43a9b5u && L < 0) p.out[0] = 0;
+  }
+  const EpiRglruGates ep{};
+  uint32_t* al = an[wave];
+  u16* ol = reinterpret_cast<u16*>(ob[wave]);
+  int bf = 0;
+  for (int c = 0; c < nch; ++c) {
+    // chunk c's DMA (issued two chunks ago) retired: only the NDMA younger
+    // pieces of chunk c + 1 stay in flight; then every wave's, by the barrier
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NDMA) : "memory");
+    __syncthreads();
+    f32x4 acc[RF][4];
+#pragma unroll
+    for (int i = 0; i < RF; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 af[RF];
+#pragma unroll
+      for (int i = 0; i < RF; ++i) {
+        const int r = 16 * i + (lane & 15), cc = 4 * ks + (lane >> 4);
+        af[i] = __builtin_bit_cast(bf16x8, xs[bf][r * CPR + (cc ^ (r & SWM))]);
+      }
+#pragma unroll
+      for (int i = 0; i < RF; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              af[i], __builtin_bit_cast(bf16x8, wf[j][ks]), acc[i][j], 0, 0, 0);
+    }
+    // gate chain of rows 16 i + 4 (lane / 16) + r, channels ch0 / ch0 + 16
+    // (rows past the sequence: the clamped last row's values, never scanned)
+    const u16* xl = reinterpret_cast<const u16*>(xs[bf]);
+#pragma unroll
+    for (int i = 0; i < RF; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = 16 * i + 4 * (lane >> 4) + r;
+        const f32x2 xv{bf2f(xl[(rl * CPR + ((ch0 >> 3) ^ (rl & SWM))) * 8 + (ch0 & 7)]),
+                       bf2f(xl[(rl * CPR + (((ch0 + 16) >> 3) ^ (rl & SWM))) * 8 + (ch0 & 7)])};
+        f32x2 av, nx;
+        ep.chain2(badd2(rbf2(f32x2{acc[i][0][r], acc[i][1][r]}), bx),
+                  badd2(rbf2(f32x2{acc[i][2][r], acc[i][3][r]}), ba), xv, sp,
+                  rs_[min(c * RT + rl, L - 1)] != 0, av, nx);
+        const uint32_t ab = pk2bf(av), nb = pk2bf(nx);
+        al[rl * AS + (lane & 15)] = (ab & 0xffffu) | (nb << 16);
+        al[rl * AS + (lane & 15) + 16] = (ab >> 16) | (nb & 0xffff0000u);
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    // the scan: lane c < 32 carries channel 32 wih + c through the chunk
+    // (a full chunk unrolled, so its LDS reads issue ahead of the chain)
+    const int nr = min(RT, L - c * RT);
+    if (lane < 32) {
+      const u16* yl = reinterpret_cast<const u16*>(ys[bf]) + 32 * wave + lane;
+      auto step = [&](int r) {
+        const uint32_t v = al[r * AS + lane];
+        h = add_rn(mul_rn(__uint_as_float(v << 16), h), __uint_as_float(v & 0xffff0000u));
+        float y = rbf(h);
+        if constexpr (GATE) y = bmul(y, bf2f(yl[r * 128]));
+        ol[r * 32 + lane] = f2bf(y);
+      };
+      if (nr == RT) {
+#pragma unroll
+        for (int r = 0; r < RT; ++r) step(r);
+      } else {
+        for (int r = 0; r < nr; ++r) step(r);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    // RT rows x 32 channels out: lane l stores 16 B of rows l / 4 (+ 16)
+#pragma unroll
+    for (int k = 0; k < RF; ++k) {
+      const int r = 16 * k + (lane >> 2), cc = lane & 3;
+      if (r < nr)
+        st16(p.out + (row0 + c * RT + r) * p.ldo + g * BW + 32 * wih + 8 * cc, ob[wave][r * 4 + cc]);
+    }
+    // chunk c + 2 into the buffers chunk c - 1 used (every wave passed this
+    // chunk's barrier after its last read of them); always issued (clamped
+    // past the end) so the counted wait above sees NDMA per chunk
+    dma(c + 2, bf == 0 ? 2 : bf - 1);
+    bf = bf == NB - 1 ? 0 : bf + 1;
+  }
+  // no LDS-DMA may still land once the workgroup's LDS is handed on
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (p.h_last && lane < 32) p.h_last[(int64_t)b * p.E + es] = h;
+}
+
 // torch.argmax order: NaN beats every number, ties (and NaN vs NaN) go to
 // the lowest index -- a NaN row still yields an index inside the vocabulary
 CADENCE_DEV bool argmax_better(float ov, int oi, float v, int i) {
@@ -2727,7 +2952,7 @@ __attribute__((visibility("hidden"))) int cadence_engine_bits() { return g_engin
 
 extern "C" {
 
-int cadence_abi_version(void) { return 15; }
+int cadence_abi_version(void) { return 16; }
 
 int cadence_gemm_set_engine(int engine) {
   const int prev = g_engine;
@@ -3067,6 +3292,51 @@ int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
   return launch_gemm(static_cast<const u16*>(X), ldx,
                      static_cast<const u16*>(Wpacked), ldw, M, 2 * bw, bw, heads,
                      bw, 2 * bw * bw, epi, workspace, ws_bytes, st);
+}
+
+// Fused prefill gates + scan plan: block widths with a 128-channel split
+// (128, 256), row-major packed weights, enough (sequence, block half) units
+// to fill the chip (the sequential walk over L is each workgroup's latency),
+// 16-B aligned rows.
+static bool rglru_scan_plan(const void* X, int64_t ldx, const void* gate, int64_t ldg,
+                            int64_t ldo, int64_t B, int64_t L, int64_t heads, int64_t bw) {
+  return (bw == 128 || bw == 256) && L >= 16 && L <= kRglruScanMaxL &&
+         B * heads * (bw / 128) >= 512 &&
+         ldx % 8 == 0 && ldo % 8 == 0 && (gate == nullptr || ldg % 8 == 0) &&
+         reinterpret_cast<uintptr_t>(X) % 16 == 0 &&
+         reinterpret_cast<uintptr_t>(gate) % 16 == 0;
+}
+
+int cadence_rglru_scan_plan(const void* X, int64_t ldx, const void* gate, int64_t ldg,
+                            int64_t ldo, int64_t B, int64_t L, int64_t heads, int64_t bw) {
+  return rglru_scan_plan(X, ldx, gate, ldg, ldo, B, L, heads, bw) ? 1 : 0;
+}
+
+int cadence_rglru_scan(const void* X, int64_t ldx, const void* Wpacked,
+                       const void* bias_x, const void* bias_a, const void* softplus_a,
+                       const int32_t* segment_pos, const float* h0, const void* gate,
+                       int64_t ldg, void* out, int64_t ldo, float* h_last, int64_t B,
+                       int64_t L, int64_t heads, int64_t bw, void* stream) {
+  if (!rglru_scan_plan(X, ldx, gate, ldg, ldo, B, L, heads, bw) ||
+      B * L > INT32_MAX || heads * bw > INT32_MAX)
+    return (int)hipErrorInvalidValue;
+  RglruScanArgs a{static_cast<const u16*>(X), ldx, static_cast<const u16*>(Wpacked),
+                  static_cast<const u16*>(bias_x), static_cast<const u16*>(bias_a),
+                  static_cast<const u16*>(softplus_a), segment_pos, h0,
+                  static_cast<const u16*>(gate), ldg, static_cast<u16*>(out), ldo, h_last,
+                  (int)B, (int)L, (int)(heads * bw), (int)heads};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)((B * heads + 7) / 8 * 16));
+  // 16-step chunks at BW 256 (its K = 256 weight fragments take 128 VGPRs;
+  // a 32-row tile's accumulators would spill), 32-step chunks at BW 128
+  if (bw == 256) {
+    if (gate) hipLaunchKernelGGL((rglru_scan_fused_kernel<256, true, 16>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((rglru_scan_fused_kernel<256, false, 16>), grid, dim3(256), 0, st, a);
+  } else {
+    if (gate) hipLaunchKernelGGL((rglru_scan_fused_kernel<128, true, 32>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((rglru_scan_fused_kernel<128, false, 32>), grid, dim3(256), 0, st, a);
+  }
+  return (int)hipGetLastError();
 }
 
 int cadence_rglru_step(const void* X, int64_t ldx, const void* Wpacked,

@@ -217,6 +217,29 @@ int cadence_rglru_gates(const void* X, int64_t ldx, const void* Wpacked,
 int cadence_rglru_gates_stream_plan(const void* X, int64_t ldx, const void* Wpacked,
                                     int64_t ldw, int64_t ldo, int64_t M, int64_t bw);
 
+/* Prefill RG-LRU with the scan fused in: cadence_rglru_gates (row-major
+ * packed weights) followed by cadence_rnn_scan (no segment_pos: the resets
+ * are already in a) in one launch, bitwise equal to the two:
+ *   a, nx = gate chain of X (layers.py:321-365);
+ *   h_t = a_t h_{t-1} + nx_t (fp32, from h0 or 0);  out = bf16(h) [* gate]
+ * (layers.py:145-199; the `x * y` join of modules.py:652 when gate != NULL).
+ * X, gate, out are [B * L] rows (sequence-major); h0 / h_last [B][heads*bw]
+ * fp32 (either may be NULL).  Only where cadence_rglru_scan_plan says 1
+ * (bw 128 / 256, enough sequences x blocks to fill the chip, aligned rows);
+ * otherwise returns hipErrorInvalidValue without launching.
+ * Replaces layers.py:345-375 + 145-199 in RecurrentBlock (modules.py:644-652). */
+int cadence_rglru_scan(const void* X, int64_t ldx, const void* Wpacked,
+                       const void* bias_x, const void* bias_a, const void* softplus_a,
+                       const int32_t* segment_pos, const float* h0, const void* gate,
+                       int64_t ldg, void* out, int64_t ldo, float* h_last, int64_t B,
+                       int64_t L, int64_t heads, int64_t bw, void* stream);
+
+/* Plan query (host only, no GPU work): 1 when cadence_rglru_scan accepts
+ * these operands. */
+int cadence_rglru_scan_plan(const void* X, int64_t ldx, const void* gate, int64_t ldg,
+                            int64_t ldo, int64_t B, int64_t L, int64_t heads,
+                            int64_t bw);
+
 /* Single-token RG-LRU step (decode, T = 1): the gate GEMM + chain of
  * cadence_rglru_gates with the scan step of rnn_scan's T == 1 branch fused
  * into the epilogue (layers.py:175-182, modules.py:652):
