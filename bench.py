@@ -531,6 +531,12 @@ def run(args):
     from cadence import _lib
     _lib.load().cadence_gemm_set_engine(args.gemm_engine)
   cfg, vis, model = build_model(dev, args.image_size, args.text_only)
+  if os.environ.get("CADENCE_DUMP_MAPS"):
+    # crash forensics (tools/pmc_crash_repro.sh): the process's library map,
+    # once every library is loaded, so a native backtrace's addresses can be
+    # resolved offline against the same image's libraries
+    with open("/proc/self/maps") as fi, open(os.environ["CADENCE_DUMP_MAPS"], "w") as fo:
+      fo.write(fi.read())
   n_vis = 0 if vis is None else vis.n_visual_tokens
   strong = bool(args.global_batch)
   gb = args.global_batch if strong else args.batch * world

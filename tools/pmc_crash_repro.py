@@ -13,6 +13,9 @@ one:
   nocopy    blocking pageable copies instead of the pinned async ones
   nograph   eager kernels instead of the graph replays
   noevent   no lane events (the caller's stream joins the lanes at the end)
+  deep      full, with a 128-kernel captured graph per lane (the decode
+            step's shape: ~130 short launches per replay), 32 replays per
+            micro-batch
   pace      full + the round-4 host pacing: before queueing on a lane the host
             synchronizes that lane's previous timing event (recorded after
             its "prefill", while the other lane replays its graph)
@@ -44,12 +47,17 @@ def main():
     x = torch.randn(32, 1024, device=dev, dtype=torch.bfloat16)
     cap = torch.cuda.Stream()
     cap.wait_stream(torch.cuda.current_stream())
+    def body():
+      if mode == "deep":                 # ~130 short kernels, like a decode step
+        for _ in range(64):
+          x.mul_(0.999).add_(1e-3)
+      y = torch.tanh(x @ w)
+      x.copy_(y)
     with torch.cuda.stream(cap):
-      y = torch.tanh(x @ w)              # warm-up
+      body()                             # warm-up
       g = torch.cuda.CUDAGraph()
       with torch.cuda.graph(g, stream=cap):
-        y = torch.tanh(x @ w)
-        x.copy_(y)
+        body()
     torch.cuda.current_stream().wait_stream(cap)
     graphs.append(g)
     statics.append(x)
@@ -75,7 +83,7 @@ def main():
       if mode == "pace":
         pace[j] = torch.cuda.Event(enable_timing=True)
         pace[j].record(ln)
-      for _ in range(8):                                  # "decode"
+      for _ in range(32 if mode == "deep" else 8):        # "decode"
         if mode == "nograph":
           statics[j].copy_(torch.tanh(statics[j] @ w))
         else:

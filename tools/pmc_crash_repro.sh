@@ -10,6 +10,7 @@ export PYTHONFAULTHANDLER=1
 $S 120 ${tag}_repro_plain.log python -u tools/pmc_crash_repro.py $mode || exit 1
 $S 120 ${tag}_repro_pmc.log rocprofv3 --pmc FETCH_SIZE --output-format csv \
    -d gpurun_out/${tag}_repro -o run -- python3 -u tools/pmc_crash_repro.py $mode || exit 1
+export CADENCE_DUMP_MAPS=gpurun_out/${tag}_bench_pmc_maps.txt
 $S 240 ${tag}_bench_pmc.log rocprofv3 --pmc FETCH_SIZE --kernel-include-regex gemm_w4 \
    --output-format csv -d gpurun_out/${tag}_bench_pmc -o run -- python3 -u bench.py \
    --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-timing || exit 1

@@ -6,14 +6,16 @@
 # usage: tools/pmc_traffic.sh TAG REGEX   -> gpurun_out/TAG/pmc_*.csv
 set -o pipefail
 export TMPDIR=/tmp
-# rocprofv3's PMC mode segfaults in the runtime (hipEventRecord /
-# device_synchronize) with the sampler's asynchronous pinned prompt copies;
-# the blocking copy changes no kernel (round 4)
-export CADENCE_SYNC_H2D=1
+# (round 4 ran these passes with CADENCE_SYNC_H2D=1 after rocprofv3's PMC
+# mode crashed in hipEventRecord; round 5 runs the bench's default path:
+# the crash did not reproduce -- DESIGN.md, "The rocprofv3 PMC crash")
 tag=${1:?tag}; rx=${2:?regex}
 out=gpurun_out/$tag
 mkdir -p $out
+export PYTHONFAULTHANDLER=1
 for c in FETCH_SIZE WRITE_SIZE; do
+  # the library map of each pass's process, for resolving a crash backtrace
+  export CADENCE_DUMP_MAPS=$out/pmc_${c}_maps.txt
   timeout -s KILL 240 rocprofv3 --pmc $c --kernel-include-regex "$rx" --output-format csv \
       -d $out/pmc_$c -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline \
       --no-kernel-timing > $out/pmc_$c.log 2>&1 || { tail -20 $out/pmc_$c.log; exit 1; }
