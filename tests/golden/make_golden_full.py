@@ -59,7 +59,7 @@ CONFIGS = {
     "c3": (224, 1, 64, 8, 203),
     "bench224": (224, 2, 64, 8, 262),
     "c4": (336, 1, 64, 8, 313),
-    "p0": (384, 1, 16, 8, 434),
+    "p0": (384, 1, 16, 8, 440),
 }
 
 
