@@ -57,7 +57,7 @@ CONFIGS = {
     "c1": (None, 1, 16, 8, 101),
     "c2": (None, 1, 2048, 8, 101),
     "c3": (224, 1, 64, 8, 203),
-    "bench224": (224, 2, 64, 8, 262),
+    "bench224": (224, 2, 64, 8, 287),
     "c4": (336, 1, 64, 8, 313),
     "p0": (384, 1, 16, 8, 440),
 }

@@ -101,3 +101,25 @@ def test_full_fixture_discriminating(name):
     assert len(set(toks)) >= 3, (name, i, toks)
     mg = f["logit_margin"][i]
     assert float(((mg >= 0.3) & (mg <= 3.0)).float().mean()) >= 1 / 3, (name, i, mg.tolist())
+
+
+def test_full_fixtures_margin_decided():
+  """Enough fixture rows hold the HIP path's argmax to exact equality
+  (VERDICT r04): a row (the prefill's last position or one decode step of
+  one sample) is held to it where the oracle's top-1 / top-2 margin exceeds
+  test_full_size_gpu._margin_bar -- max(0.2, 1.5x the bf16 oracle's own
+  max-abs distance from its fp32 run on that row).  At least two thirds of
+  all rows and at least 5 of c3's 9 (the fixture weight seeds are chosen by
+  tests/golden/seed_search.py; the bars themselves are unchanged)."""
+  from test_full_size_gpu import _margin_bar
+  counts = {}
+  for name in MG.CONFIGS:
+    f = load_file(os.path.join(HERE, "golden", f"full_{name}.safetensors"))
+    b, rows = f["logit_margin"].shape
+    n = sum(float(f["logit_margin"][i, j]) > _margin_bar(f, i, j)
+            for i in range(b) for j in range(rows))
+    counts[name] = (n, b * rows)
+  enforced = sum(n for n, _ in counts.values())
+  total = sum(t for _, t in counts.values())
+  assert 3 * enforced >= 2 * total, counts
+  assert counts["c3"][0] >= 5, counts
