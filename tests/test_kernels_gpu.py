@@ -595,7 +595,9 @@ def test_kv_cache_fill_and_decode(dev):
                                     (581, 16, 64), (576, 16, 72), (734, 16, 64),
                                     (729, 16, 72), (300, 3, 72), (289, 2, 64),
                                     (1, 2, 72), (64, 3, 72), (65, 2, 72), (320, 2, 64),
-                                    (385, 1, 64), (129, 5, 72)])
+                                    (385, 1, 64), (129, 5, 72), (40, 2, 64),
+                                    (100, 3, 64), (129, 2, 64), (1, 2, 64),
+                                    (288, 2, 64)])
 def test_vit_attention(dev, n, h, hd):
   """timm SDPA (fp32) vs the LDS-resident kernel (hd 64, N <= 288) and the
   streaming kernel vit_flash_attn_kernel (everything else: SigLIP 224 px,
