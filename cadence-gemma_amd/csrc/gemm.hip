@@ -2712,6 +2712,26 @@ bool use_w4(int64_t N, int64_t K, int rows) {
   return (g_engine & 1) && K >= 2048 && N >= 8192 && (rows == 224 || rows == 256);
 }
 
+// Tile height of the 4-wave engine: 256 rows up to kW4TallMaxM rows of A,
+// 224 beyond (its round-count model picks 256 at C2's M = 65536 and 224 at
+// the bench's 10208, the opposite of what runs faster).  Measured at the gated MLP shape
+// (N = 15360, K = 2560; profiles/r05k_w4_tile_rows.log): M = 10208 (the
+// bench) 642 vs 650-652 us in the bench pipeline (734.9-735.8 vs 739.0-739.9
+// ms per step) and 687-691 vs 703 us isolated, M = 20448 (C4) 1343-1350 vs
+// 1381-1388 us, but M = 65536 (C2) 4320-4334 vs 4209-4213 us for 224 rows.
+// CADENCE_W4_ROWS = 224 / 256 forces one (lab A/B).
+constexpr int64_t kW4TallMaxM = 32768;
+int w4_tile_rows(int64_t M, int rows) {
+  static const int forced = [] {
+    const char* e = getenv("CADENCE_W4_ROWS");
+    const int r = e ? atoi(e) : 0;
+    return (r == 224 || r == 256) ? r : 0;
+  }();
+  if (forced) return forced;
+  (void)rows;
+  return M <= kW4TallMaxM ? 256 : 224;
+}
+
 // Prefill engine plan for M > kSkinnyMaxM: 0 = 2-buffer 256-row kernel,
 // 160 / 192 / 224 / 256 = 8-phase kernel with that tile height.
 //  * 8-phase when K splits into pairs of 64-deep tiles (an A/B of the
@@ -2822,11 +2842,12 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
       return (int)hipGetLastError();
     }
     if (use_w4(N, K, rows)) {
-      const dim3 wgrid((unsigned)(((M + rows - 1) / rows) * ((N + 255) / 256)),
+      const int wrows = w4_tile_rows(M, rows);
+      const dim3 wgrid((unsigned)(((M + wrows - 1) / wrows) * ((N + 255) / 256)),
                        (unsigned)groups);
       if constexpr (std::is_same_v<Epi, EpiLinear>) {
 #define CADENCE_W4_ACT(ACT_)                                                              \
-  if (rows == 224)                                                                        \
+  if (wrows == 224)                                                                       \
     hipLaunchKernelGGL((gemm_w4_kernel<EpiLinearA<ACT_>, 7>), wgrid, dim3(256), 0, st, A,   \
                        lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff,               \
                        EpiLinearA<ACT_>{epi});                                            \
@@ -2842,7 +2863,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
           default: return (int)hipErrorInvalidValue;
         }
 #undef CADENCE_W4_ACT
-      } else if (rows == 224) {
+      } else if (wrows == 224) {
         hipLaunchKernelGGL((gemm_w4_kernel<Epi, 7>), wgrid, dim3(256), 0, st, A, lda, W, ldw,
                            (int)M, (int)N, (int)K, a_goff, w_goff, epi);
       } else {
@@ -2976,7 +2997,9 @@ int cadence_gemm_engine(int64_t M, int64_t N, int64_t K, int64_t groups) {
 
 int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
   if (M <= kSkinnyMaxM || M <= 0) return 0;
-  const int r = big_tile_rows(M, N, K, groups > 0 ? groups : 1);
+  const int64_t g = groups > 0 ? groups : 1;
+  const int r = big_tile_rows(M, N, K, g);
+  if (big_splits(M, N, K, g, r) == 1 && use_w4(N, K, r)) return w4_tile_rows(M, r);
   return r ? r : 256;
 }
 

@@ -174,7 +174,8 @@ def test_prefill_gemm_plan_host_arithmetic():
   heights DESIGN §4 names, one-image / one-prompt shapes split K."""
   lib = _lib.load()
   rows = lib.cadence_gemm_tile_rows
-  assert rows(32 * 319, 15360, 2560, 1) == 224        # Griffin gated MLP
+  assert rows(32 * 319, 15360, 2560, 1) == 256        # Griffin gated MLP (4-wave engine)
+  assert rows(32 * 2048, 15360, 2560, 1) == 224       # C2's gated MLP (4-wave engine)
   assert rows(32 * 319, 2560, 7680, 1) == 224         # Griffin down projection
   assert rows(32 * 261, 1024, 1024, 1) == 160         # DINO attention proj
   assert rows(32 * 256, 1152, 1152, 1) == 192         # SigLIP attention proj

@@ -27,6 +27,10 @@ KEYS = {
         r"gemm_w4_kernel<[^>]*EpiGatedGelu, 7>",
         2 * (10208 * 2560 + 2 * 7680 * 2560 + 10208 * 7680),
         "A (M x K) + W (2F x K) + out (M x F), bf16"),
+    "gemm_w4_kernel<EpiGatedGelu, 8>": (
+        r"gemm_w4_kernel<[^>]*EpiGatedGelu, 8>",
+        2 * (10208 * 2560 + 2 * 7680 * 2560 + 10208 * 7680),
+        "A (M x K) + W (2F x K) + out (M x F), bf16"),
     "rglru_scan_fused_kernel<256>": (
         r"rglru_scan_fused_kernel<256", 6 * 10208 * 2560 + 10 * 512 * 256 * 2
         + 32 * 2560 * 4 + 10208 * 4,
