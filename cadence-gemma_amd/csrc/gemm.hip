@@ -2755,6 +2755,14 @@ int big_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
     return n;
   }();
   if (K % (2 * BK) != 0) return 0;
+  // lab A/B: CADENCE_TILE_ROWS = 160 / 192 / 224 / 256 forces the block
+  // engine's tile height for every shape
+  static const int forced = [] {
+    const char* e = getenv("CADENCE_TILE_ROWS");
+    const int r = e ? atoi(e) : 0;
+    return (r == 160 || r == 192 || r == 224 || r == 256) ? r : 0;
+  }();
+  if (forced) return forced;
   const int64_t ntn = (N + 255) / 256;
   auto rounds = [&](int64_t bm) {
     const int64_t t = ((M + bm - 1) / bm) * ntn * groups;
