@@ -2721,14 +2721,13 @@ bool use_w4(int64_t N, int64_t K, int rows) {
 // 1381-1388 us, but M = 65536 (C2) 4320-4334 vs 4209-4213 us for 224 rows.
 // CADENCE_W4_ROWS = 224 / 256 forces one (lab A/B).
 constexpr int64_t kW4TallMaxM = 32768;
-int w4_tile_rows(int64_t M, int rows) {
+int w4_tile_rows(int64_t M) {
   static const int forced = [] {
     const char* e = getenv("CADENCE_W4_ROWS");
     const int r = e ? atoi(e) : 0;
     return (r == 224 || r == 256) ? r : 0;
   }();
   if (forced) return forced;
-  (void)rows;
   return M <= kW4TallMaxM ? 256 : 224;
 }
 
@@ -2850,7 +2849,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
       return (int)hipGetLastError();
     }
     if (use_w4(N, K, rows)) {
-      const int wrows = w4_tile_rows(M, rows);
+      const int wrows = w4_tile_rows(M);
       const dim3 wgrid((unsigned)(((M + wrows - 1) / wrows) * ((N + 255) / 256)),
                        (unsigned)groups);
       if constexpr (std::is_same_v<Epi, EpiLinear>) {
@@ -3007,7 +3006,7 @@ int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
   if (M <= kSkinnyMaxM || M <= 0) return 0;
   const int64_t g = groups > 0 ? groups : 1;
   const int r = big_tile_rows(M, N, K, g);
-  if (big_splits(M, N, K, g, r) == 1 && use_w4(N, K, r)) return w4_tile_rows(M, r);
+  if (big_splits(M, N, K, g, r) == 1 && use_w4(N, K, r)) return w4_tile_rows(M);
   return r ? r : 256;
 }
 
