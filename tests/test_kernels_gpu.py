@@ -614,6 +614,21 @@ def test_vit_attention(dev, n, h, hd):
   assert cosine(got, want) > 0.9999
 
 
+@pytest.mark.parametrize("m,d", [(32 * 261, 1024), (32 * 256, 1152), (7, 1024),
+                                 (13, 1152), (4, 64), (5, 1280), (3, 2048)])
+def test_layernorm(dev, m, d):
+  """The ViT LayerNorm (fp32 residual rows in, bf16 out; timm's eps 1e-6)
+  against torch's fp32 layer_norm: the register form (rows up to 1280
+  wide) and the looped one beyond, ragged row counts."""
+  g = torch.Generator().manual_seed(29)
+  x = (torch.randn(m, d, generator=g) * 3 + 0.5).to(dev)
+  w = (torch.randn(d, generator=g) * 0.5 + 1).to(torch.bfloat16).to(dev)
+  b = (torch.randn(d, generator=g) * 0.2).to(torch.bfloat16).to(dev)
+  got = ops.ops.layernorm(x, w, b, 1e-6)
+  want = torch.nn.functional.layer_norm(x.cpu(), (d,), w.float().cpu(), b.float().cpu(), 1e-6)
+  assert rel_l2(got.float().cpu(), want) < 4e-3
+
+
 # --------------------------------------------------------------- others
 
 def test_embed_and_logits_argmax(dev):
