@@ -2709,7 +2709,13 @@ int g_engine = 15;
 // Short K keeps the 8-wave engine, whose 8 waves also finish element-wise
 // epilogues twice as fast (fc1's erf-GELU at K = 1024: 0.87x on 4 waves).
 bool use_w4(int64_t N, int64_t K, int rows) {
-  return (g_engine & 1) && K >= 2048 && N >= 8192 && (rows == 224 || rows == 256);
+  // lab A/B: CADENCE_W4_MIN_N lowers the N threshold
+  static const int64_t min_n = [] {
+    const char* e = getenv("CADENCE_W4_MIN_N");
+    const long v = e ? atol(e) : 0;
+    return (int64_t)(v > 0 ? v : 8192);
+  }();
+  return (g_engine & 1) && K >= 2048 && N >= min_n && (rows == 224 || rows == 256);
 }
 
 // Tile height of the 4-wave engine: 256 rows up to kW4TallMaxM rows of A,
@@ -2721,13 +2727,14 @@ bool use_w4(int64_t N, int64_t K, int rows) {
 // 1381-1388 us, but M = 65536 (C2) 4320-4334 vs 4209-4213 us for 224 rows.
 // CADENCE_W4_ROWS = 224 / 256 forces one (lab A/B).
 constexpr int64_t kW4TallMaxM = 32768;
-int w4_tile_rows(int64_t M) {
+int w4_tile_rows(int64_t M, int64_t N) {
   static const int forced = [] {
     const char* e = getenv("CADENCE_W4_ROWS");
     const int r = e ? atoi(e) : 0;
     return (r == 224 || r == 256) ? r : 0;
   }();
   if (forced) return forced;
+  if (N < 8192) return 224;   // the narrower projections (lab: CADENCE_W4_MIN_N)
   return M <= kW4TallMaxM ? 256 : 224;
 }
 
@@ -2849,7 +2856,7 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
       return (int)hipGetLastError();
     }
     if (use_w4(N, K, rows)) {
-      const int wrows = w4_tile_rows(M);
+      const int wrows = w4_tile_rows(M, N);
       const dim3 wgrid((unsigned)(((M + wrows - 1) / wrows) * ((N + 255) / 256)),
                        (unsigned)groups);
       if constexpr (std::is_same_v<Epi, EpiLinear>) {
@@ -2862,12 +2869,16 @@ int launch_gemm(const u16* A, int64_t lda, const u16* W, int64_t ldw, int64_t M,
     hipLaunchKernelGGL((gemm_w4_kernel<EpiLinearA<ACT_>, 8>), wgrid, dim3(256), 0, st, A,   \
                        lda, W, ldw, (int)M, (int)N, (int)K, a_goff, w_goff,               \
                        EpiLinearA<ACT_>{epi})
-        switch (epi.act) {
-          case 0: CADENCE_W4_ACT(0); break;
-          case 1: CADENCE_W4_ACT(1); break;
-          case 2: CADENCE_W4_ACT(2); break;
-          case 3: CADENCE_W4_ACT(3); break;
-          default: return (int)hipErrorInvalidValue;
+        if (epi.act == 0 && epi.resid && (g_engine & 4)) {
+          CADENCE_W4_ACT(4);
+        } else {
+          switch (epi.act) {
+            case 0: CADENCE_W4_ACT(0); break;
+            case 1: CADENCE_W4_ACT(1); break;
+            case 2: CADENCE_W4_ACT(2); break;
+            case 3: CADENCE_W4_ACT(3); break;
+            default: return (int)hipErrorInvalidValue;
+          }
         }
 #undef CADENCE_W4_ACT
       } else if (wrows == 224) {
@@ -3006,7 +3017,7 @@ int cadence_gemm_tile_rows(int64_t M, int64_t N, int64_t K, int64_t groups) {
   if (M <= kSkinnyMaxM || M <= 0) return 0;
   const int64_t g = groups > 0 ? groups : 1;
   const int r = big_tile_rows(M, N, K, g);
-  if (big_splits(M, N, K, g, r) == 1 && use_w4(N, K, r)) return w4_tile_rows(M);
+  if (big_splits(M, N, K, g, r) == 1 && use_w4(N, K, r)) return w4_tile_rows(M, N);
   return r ? r : 256;
 }
 
