@@ -387,6 +387,21 @@ int main() {
   run_split<8, 3, 2, 1>(L, 2560, 2560, 4);
   run_pipe<16, 5, 1, 1, 5>(L, "pipe nw16 nrep1 ch1x5 unsplit (160 wg)", 2560, 2560);
   run_shipped<5>(L, "shipped stream<32,5,2> S2 combine (160 wg)", 2560, 2560, 2);
+  // round 5: more waves in flight (two or four workgroups per CU), after the
+  // pure reads above reached their rate only at 2048 x 4 waves
+  printf("== occupancy sweep: down projection\n");
+  run_shipped<10>(L, "shipped stream<32,10,2> S3 combine (240 wg)", 2560, 7680, 3);
+  run_split<8, 5, 2, 2>(L, 2560, 7680, 6);
+  run_split<8, 4, 2, 2>(L, 2560, 7680, 8);
+  run_split<16, 5, 2, 1>(L, 2560, 7680, 3);
+  run_split<16, 3, 2, 1>(L, 2560, 7680, 5);
+  run_split<8, 4, 1, 2>(L, 2560, 7680, 8);
+  printf("== occupancy sweep: out projection\n");
+  run_pipe<16, 5, 1, 1, 5>(L, "pipe nw16 nrep1 ch1x5 unsplit (160 wg)", 2560, 2560);
+  run_split<8, 5, 2, 2>(L, 2560, 2560, 2);
+  run_split<8, 3, 1, 2>(L, 2560, 2560, 4);
+  run_split<4, 5, 1, 4>(L, 2560, 2560, 4);
+  run_split<8, 2, 1, 2>(L, 2560, 2560, 5);
   printf("done\n");
   return 0;
 }
