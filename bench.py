@@ -40,6 +40,32 @@ METRIC = ("multimodal prefill+decode tokens/sec, Cadence-2B 224px bs=32, "
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_BF16_PEAK_TFS = 2500.0    # dense bf16 MFMA spec
 
+# Where a key's meaning changed between rounds (lines of different rounds are
+# comparable only where the version matches).
+DEFINITIONS = {
+    "version": 6,
+    "prefill_tokens_per_s": "aggregate over ranks since round 5 (per rank before)",
+    "value (config c3)": "one request at a time since round 5 (two requests in "
+                         "flight before; that rate is value_serving now)",
+    "roofline_scan": "the RG-LRU scan kernel the workload runs since round 6 "
+                     "(rglru_scan_fused_kernel at the headline shape); the "
+                     "isolated rnn_scan_kernel figure is roofline_scan_isolated",
+}
+
+
+def scaling_inputs(world, gb, tok_per_step, ms_step, rank_ms, rank_prefill_ms,
+                   prefill_tps):
+  """The quantities a 1 -> N speed-up is computed from, on both the
+  end-to-end value and the prefill rate: each rank's own wall time per step
+  (its share gb / world of the global batch), the slowest of them (what
+  `value` divides by), and each rank's timed prefill."""
+  return {"world": world, "global_batch": gb, "samples_per_rank": gb // world,
+          "tokens_per_step": tok_per_step,
+          "end_to_end_ms_per_step": round(ms_step, 3),
+          "end_to_end_ms_per_step_by_rank": [round(v, 3) for v in rank_ms],
+          "prefill_ms_by_rank": [round(v, 3) for v in rank_prefill_ms],
+          "prefill_tokens_per_s": round(prefill_tps, 1)}
+
 
 class BenchVocab:
   """Synthetic token ids only; the Gemma tokenizer is not shipped."""
@@ -462,10 +488,14 @@ def rehearse(args):
       tp = time.perf_counter() - t1
     out = D.gather_rows(torch.cat(outs))
   D.barrier()
-  elapsed = D.max_over_ranks(time.perf_counter() - t0)
+  own = time.perf_counter() - t0
+  elapsed = D.max_over_ranks(own)
+  rank_ms = D.all_over_ranks(own / args.steps * 1e3)
+  rank_prefill_ms = D.all_over_ranks(tp * 1e3)
   mb = micro[0].stop - micro[0].start
   agg, per = prefill_rates(mb, n_vis + args.prompt, D.max_over_ranks(tp) * 1e3 + 1e-6,
                            world)
+  tok_per_step = gb * (n_vis + args.prompt + args.decode)
   if rank == 0:
     print(json.dumps({
         "metric": "rehearsal (CPU, no model): " + METRIC, "n_gpus": world,
@@ -476,6 +506,10 @@ def rehearse(args):
                    "parallelism": f"dp{world}"},
         "prefill_tokens_per_s": round(agg, 1),
         "prefill_tokens_per_s_per_rank": round(per, 1),
+        "scaling_inputs": scaling_inputs(world, gb, tok_per_step,
+                                         elapsed / args.steps * 1e3, rank_ms,
+                                         rank_prefill_ms, agg),
+        "definitions": DEFINITIONS,
         "generated_tokens_checksum": int(out.long().sum().item()),
         "gathered_rows": int(out.shape[0])}), flush=True)
   D.barrier()
@@ -766,7 +800,13 @@ def run(args):
   prefill_tps, prefill_tps_rank = prefill_rates(
       mb, n_vis + args.prompt - (1 if args.decode else 0), pre_ms, world)
 
+  # every rank's own end-to-end time per step (the driver's speed-up input
+  # on `value`) and its prefill time, gathered before rank 0 prints
+  rank_ms = D.all_over_ranks(dt / args.steps * 1e3)
+  rank_prefill_ms = D.all_over_ranks(sum(prefill_ms) / max(len(prefill_ms), 1))
   result = None
+  fused_scan = next((roofline_entry(ksum, k, "hbm", args.config) for k in sorted(ksum)
+                     if k.startswith("rglru_scan_fused_kernel")), None)
   if rank == 0:
     # dominant kernel: the single-stream GEMM key with the most time in the
     # step (ViT-tower launches share the GPU between two streams: their keys
@@ -846,15 +886,21 @@ def run(args):
         "prefill_tokens_per_s_definition": (
             "aggregate over ranks: world x micro-batch x prefill tokens per "
             "sample / max-over-ranks prefill time of the timed micro-batch"),
+        "scaling_inputs": scaling_inputs(world, gb, tok_per_step, ms_step, rank_ms,
+                                         rank_prefill_ms, prefill_tps),
+        "definitions": DEFINITIONS,
         "roofline": roofline_entry(ksum, dom, "mfma", args.config) if dom else None,
+        # the RG-LRU scan the workload runs: the scan kernel where the
+        # headline launches it, else the fused gates + scan kernel (HBM-priced
+        # on x and the y gate in, y out, weights and state; the gate chain's
+        # VALU, not the bytes, bounds it)
         "roofline_scan": (roofline_entry(ksum, scan_key, "hbm", args.config)
-                          if scan_key else scan_iso),
-        # prefill RG-LRU gates + scan fused (one launch per recurrent block):
-        # HBM-priced on x and the y gate in, y out, weights and state; the
-        # gate chain's VALU, not the bytes, bounds it
-        "roofline_rglru_fused": next((roofline_entry(ksum, k, "hbm", args.config)
-                                      for k in sorted(ksum)
-                                      if k.startswith("rglru_scan_fused_kernel")), None),
+                          if scan_key else fused_scan),
+        "roofline_rglru_fused": fused_scan,
+        # rnn_scan_kernel alone at the workload's shape (the small-batch /
+        # rnn_scan API path), timed after the timed region: not a kernel the
+        # headline runs when roofline_scan names the fused kernel
+        "roofline_scan_isolated": scan_iso,
         "roofline_decode": dec,
         # prefill RG-LRU gates: HBM-priced (x in, a and normalised x out)
         "roofline_rglru_gates": next((roofline_entry(ksum, k, "hbm", args.config)

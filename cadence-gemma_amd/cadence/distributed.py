@@ -152,6 +152,17 @@ def max_over_ranks(value: float) -> float:
   return float(t.item())
 
 
+def all_over_ranks(value: float) -> list[float]:
+  """Every rank's `value`, in rank order (one all-gather of one float per
+  rank; [value] without a process group)."""
+  if not (dist.is_available() and dist.is_initialized()):
+    return [value]
+  dev = torch.device("cuda", torch.cuda.current_device()) \
+      if dist.get_backend() == "nccl" else torch.device("cpu")
+  t = torch.tensor([value], dtype=torch.float64, device=dev)
+  return [float(v) for v in gather_rows(t).cpu()]
+
+
 def shutdown() -> None:
   if dist.is_available() and dist.is_initialized():
     dist.destroy_process_group()

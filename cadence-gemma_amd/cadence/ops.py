@@ -601,7 +601,16 @@ def _rglru_scan(x, w_packed, bias_x, bias_a, softplus_a, segment_pos, h0, gate,
   M, E = x.shape
   H, two_bw, bw = w_packed.shape
   _need(two_bw == 2 * bw and H * bw == E and M == B * L, "w_packed / x shape")
+  # the kernel reads w_packed as a dense row-major [H][2 bw][bw] array (no
+  # leading dimension is passed) and the three gate vectors by channel
+  _need(w_packed.is_contiguous() and w_packed.dtype == _BF16,
+        "w_packed: contiguous bf16 [H, 2 bw, bw]")
+  for name, v in (("bias_x", bias_x), ("bias_a", bias_a), ("softplus_a", softplus_a)):
+    _need(v.dtype == _BF16 and v.numel() == E and v.is_contiguous(),
+          f"{name}: contiguous bf16 [E]")
   _need(segment_pos.dtype == _I32 and segment_pos.numel() == M, "segment_pos")
+  if gate is not None:
+    _need(tuple(gate.shape) == (M, E), "gate: [B * L, E]")
   ldg = _mat(gate, "gate") if gate is not None else 0
   if h0 is not None:
     _need(h0.dtype == _F32 and h0.is_contiguous() and tuple(h0.shape) == (B, E),

@@ -2039,8 +2039,14 @@ __global__ __launch_bounds__(BW * 2) void rglru_gates_stream_kernel(
 // `x * y` join of modules.py:652): the (a, normalised x) pair never goes to
 // HBM.  A workgroup owns one sequence b and 128 channels of one head block g
 // (4 waves x 32 channels) for the whole sequence, and walks it in chunks of
-// 32 time steps: the chunk's X rows (the block's BW conv outputs) and y-gate
-// rows are register-staged one chunk ahead into double LDS buffers; each
+// RT time steps (RT = 16 at BW 256, 32 at BW 128: a 32-row chunk's
+// accumulators would spill beside BW 256's weight fragments).  The chunk's X
+// rows (the block's BW conv outputs) and y-gate rows come by LDS-DMA
+// (glds16_asm, 16 B per lane) into a ring of NB = 3 chunk buffers, issued
+// two chunks ahead: every wave issues NDMA pieces per chunk, so a counted
+// vmcnt(NDMA) -- the next chunk's pieces may stay in flight -- plus a
+// barrier retires chunk c before it is read, and the buffer refilled at
+// chunk c (c + 2's) was last read at chunk c - 1, behind that barrier.  Each
 // wave runs rglru_gates_stream_kernel's MFMAs (same fragments, same k order)
 // and chain2 for its 32 channels, parks the bf16 (a, nx) pairs in its own
 // LDS slab, and its lanes 0..31 then scan the chunk's 32 steps, one channel

@@ -217,6 +217,17 @@ def test_bench_self_spawn_world2_gloo():
   assert two["gathered_rows"] == one["gathered_rows"] == 8
   assert two["config"]["micro_batches_per_gpu"] == 2
   assert two["generated_tokens_checksum"] == one["generated_tokens_checksum"]
+  # both speed-up quantities: the end-to-end value (every rank's own wall
+  # time per step, the slowest of which `value` divides by) and the
+  # aggregate prefill rate
+  for line, world in ((one, 1), (two, 2)):
+    si = line["scaling_inputs"]
+    assert si["world"] == world and si["samples_per_rank"] == 8 // world
+    assert len(si["end_to_end_ms_per_step_by_rank"]) == world
+    assert len(si["prefill_ms_by_rank"]) == world
+    assert si["end_to_end_ms_per_step"] >= max(si["end_to_end_ms_per_step_by_rank"]) - 1e-3
+    assert si["prefill_tokens_per_s"] == line["prefill_tokens_per_s"]
+    assert line["definitions"]["version"] >= 6
 
 
 def test_bench_rank_failure_exits_nonzero():

@@ -4,9 +4,9 @@ The full-size fixtures (tests/golden/make_golden_full.py) hold B <= 2, and
 at B <= 2 the model takes other kernels than the bench does (the T-chunked
 scan, split-K prefill GEMMs).  Here the same fixture samples are placed in a
 batch of 32 -- at rows 0 and 31, with hashed filler samples between them --
-so the prefill runs the kernels the headline runs (sequential
-`rnn_scan_kernel`, non-split `gemm_big_kernel` at M = 32 L, the MQA prefill
-attention over 32 sequences) and the decode runs the B = 32 hipGraph step.
+so the prefill runs the kernels the headline runs (the fused RG-LRU gates +
+scan `rglru_scan_fused_kernel`, non-split `gemm_big_kernel` at M = 32 L, the
+MQA prefill attention over 32 sequences) and the decode runs the B = 32 hipGraph step.
 Rows 0 and 31 are held to the bars of tests/test_full_size_gpu.py:
 
   * the prefill's last-position logits (final norm of the B = 32 prefill,
@@ -65,10 +65,16 @@ def _batch(name, f, dev):
 
 def _plan(L):
   """The kernels a B = 32 prefill of L tokens takes (the host-side plan
-  queries of the C ABI): the sequential scan (no chunk workspace) and the
-  non-split big GEMM for the gated MLP and the recurrent projections."""
+  queries of the C ABI): the fused RG-LRU gates + scan (the 2B preset: 10
+  heads of 256 channels; x the conv output rows, the y gate a column slice
+  of the packed [y | x] rows), the sequential scan where it is not taken (no
+  chunk workspace), and the non-split big GEMM for the gated MLP and the
+  recurrent projections."""
   lib = _lib.load()
   M = B * L
+  aligned = 1 << 12          # host-only query: any 16-B aligned address
+  assert lib.cadence_rglru_scan_plan(aligned, 2560, aligned, 5120, 2560, B, L, 10,
+                                     256) == 1, "fused RG-LRU gates + scan"
   assert lib.cadence_rnn_scan_workspace_bytes(B, L, 2560) == 0, "chunked scan"
   for n, k in ((2 * 7680, 2560), (2 * 2560, 2560), (2560, 7680)):
     assert lib.cadence_gemm_big_splits(M, n, k, 1) == 1, f"split-K at {M}x{n}x{k}"
