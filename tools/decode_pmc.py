@@ -84,15 +84,20 @@ def summary(d, out):
                   "fetch_kib": round(f_kib, 1), "write_kib": round(w_kib, 1),
                   "hbm_bytes": round(hbm), "algorithmic_bytes": alg,
                   "ratio": round(hbm / alg, 3) if alg else None}
-  part = B * D * 4   # one fp32 K-split partial of a [B, D] residual output
+  act = lambda k: 8 * B * k * 2   # packed activation rows fetched once per XCD (8 L2s)
   notes = {
       "MLP down projection, K splits combined in-kernel":
-          f"extra over the weights = {part} B per fp32 K-split partial, written and read "
-          f"back by the in-kernel combine (10 splits: 20 x {part} B = 6.6 MB)",
+          f"extra over the weights ~ the [B, F] activations once per XCD ({act(F)} B) + "
+          f"the 3 K splits' fp32 partials written and read back ({2 * 3 * B * D * 4} B) + "
+          f"the residual rows in and out ({2 * B * D * 2} B)",
       "output projections (residual epilogue)":
-          "extra = the fp32 K-split partials' round trip (B x D x 4 B per split)",
+          f"extra ~ the [B, D] activations once per XCD ({act(D)} B) + the residual "
+          f"rows in and out ({2 * B * D * 2} B)",
       "recurrent y|x projection + Conv1D step":
-          "extra = the Conv1D state (read + write) and the y / x outputs",
+          f"extra ~ the activations once per XCD ({act(D)} B), the Conv1D state read + "
+          "written and the y / x outputs",
+      "attention q|k|v projection + RoPE":
+          f"extra ~ the activations once per XCD ({act(D)} B) and the q / k / v outputs",
       "RG-LRU gates GEMV + scan step":
           "algorithmic = block-diagonal gate weights + the fp32 RG-LRU state read and "
           "written; the rest is the [B, 2E] gate inputs and outputs",
