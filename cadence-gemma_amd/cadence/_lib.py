@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # CADENCE_LIB_PATH: the host-ASan build of the same C-ABI
 # (tools/asan_host.sh, CPU-only contract tests); unset everywhere else
 LIB_PATH = os.environ.get("CADENCE_LIB_PATH") or os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -69,6 +69,7 @@ _SIGS: dict[str, list] = {
     "cadence_rmsnorm": [P, I64, P, P, I64, I64, I64, F32, P],
     "cadence_layernorm": [P, I64, P, P, P, I64, I64, I64, F32, P],
     "cadence_embed": [P, P, P, I64, I64, I64, I64, F32, I64, I64, I64, P],
+    "cadence_embed_packed": [P, P, P, I64, P, I64, I64, I64, F32, P],
     "cadence_conv1d": [P, I64, P, P, P, P, P, I64, P, I64, I64, I64, I64, I32,
                        P],
     "cadence_rnn_scan": [P, I64, P, I64, P, P, P, I64, P, I64, P, I64, I64, I64,

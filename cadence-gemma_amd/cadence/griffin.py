@@ -123,12 +123,13 @@ class Griffin(nn.Module):
     return x, pos, t
 
   def run_blocks(self, x, pos, b, length, cache, return_cache,
-                 inplace_state=False, final_norm=False):
+                 inplace_state=False, final_norm=False, xn0=None):
     """Runs the residual blocks; each block's last GEMM also produces the
-    next norm's output.  Returns (x, final_norm(x) if final_norm else None,
+    next norm's output (xn0: the first block's, e.g. the decode step's lazy
+    PackedRows).  Returns (x, final_norm(x) if final_norm else None,
     cache)."""
     new_cache = {}
-    xn = None
+    xn = xn0
     n = len(self.blocks)
     for i, block in enumerate(self.blocks):
       name = f"blocks.{i}"
@@ -181,10 +182,18 @@ class Griffin(nn.Module):
     [B, V] or None, cache).
     """
     b = tokens.shape[0]
-    x, pos, _ = self.embed_inputs(tokens.reshape(b, 1),
-                                  segment_pos.reshape(b, 1))
+    xn0 = None
+    if ops.want_packed(b, self.config.width) and tokens.is_cuda:
+      # one launch for the embedding in both layouts; the first block's
+      # decode GEMVs apply its temporal_pre_norm on load, as every later
+      # block's do (no separate RMSNorm launch)
+      x, xn0 = self.embedder.encode_packed(tokens, self.blocks[0].temporal_pre_norm)
+      pos = segment_pos.reshape(b, 1).to(torch.int32).contiguous()
+    else:
+      x, pos, _ = self.embed_inputs(tokens.reshape(b, 1),
+                                    segment_pos.reshape(b, 1))
     x, xn, new_cache = self.run_blocks(x, pos, b, 1, cache, True, inplace,
-                                       final_norm=True)
+                                       final_norm=True, xn0=xn0)
     logits, nxt = ops.logits_argmax(
         xn, self.embedder.input_embedding,
         float(self.config.logits_soft_cap or 0.0), return_logits)

@@ -456,6 +456,17 @@ class Embedder(nn.Module):
     div, mul, off = row_map if row_map is not None else (max(m, 1), 0, 0)
     ops.ops.embed_(tok, self.input_embedding, self.scale, out2d, div, mul, off)
 
+  def encode_packed(self, tokens: torch.Tensor, norm):
+    """The decode step's input rows (M <= 32): (x [M, D] row-major, the same
+    rows as PackedRows carrying `norm`, the first block's temporal_pre_norm,
+    which its decode GEMVs apply on load)."""
+    tok = tokens.reshape(-1).to(torch.int32).contiguous()
+    m, d = tok.numel(), self.embed_dim
+    x = torch.empty(m, d, dtype=self.input_embedding.dtype, device=tok.device)
+    xp = ops.packed_empty(m, d, tok.device)
+    ops.ops.embed_packed_(tok, self.input_embedding, self.scale, x, xp)
+    return x, ops.PackedRows(xp, m, d, norm, x)
+
   def encode(self, x: torch.Tensor) -> torch.Tensor:
     out = torch.empty(x.numel(), self.embed_dim, dtype=self.input_embedding.dtype,
                       device=x.device)

@@ -763,6 +763,22 @@ def _embed(tokens, embedding, scale, out, row_div, row_mul, row_off):
       _s(tokens)), "embed")
 
 
+@_reg("embed_packed_(Tensor tokens, Tensor embedding, float scale, Tensor(a!) out, "
+      "Tensor(a!) packed) -> ()")
+def _embed_packed(tokens, embedding, scale, out, packed):
+  """The decode step's embedding, row-major into `out` and in the decode
+  activation layout into `packed` (cadence_embed_packed)."""
+  _need(tokens.dtype == _I32 and tokens.is_contiguous(), "tokens int32")
+  ldo = _mat(out, "out")
+  m, d = tokens.numel(), embedding.shape[1]
+  _need(tuple(out.shape) == (m, d) and want_packed(m, d), "embed_packed: [m <= 32, d % 32]")
+  _need(packed.dtype == _BF16 and packed.is_contiguous() and
+        packed.numel() == d * 16 * (-(-m // 16)), "embed_packed: packed rows")
+  _lib.check(_lib.load().cadence_embed_packed(
+      _p(tokens), _p(embedding), _p(out), ldo, _p(packed), m, d, embedding.shape[0],
+      float(scale), _s(tokens)), "embed_packed")
+
+
 # -------------------------------------------------------- recurrent block
 
 @_reg("conv1d(Tensor x, Tensor w, Tensor b, Tensor segment_pos, Tensor? cache, "

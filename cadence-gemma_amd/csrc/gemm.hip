@@ -2997,7 +2997,7 @@ __attribute__((visibility("hidden"))) int cadence_engine_bits() { return g_engin
 
 extern "C" {
 
-int cadence_abi_version(void) { return 16; }
+int cadence_abi_version(void) { return 17; }
 
 int cadence_gemm_set_engine(int engine) {
   const int prev = g_engine;

@@ -180,7 +180,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(
 __global__ __launch_bounds__(256) void embed_kernel(
     const int32_t* __restrict__ tok, const u16* __restrict__ E,
     u16* __restrict__ out, int64_t ldo, int64_t M, int D, int64_t V,
-    float scale, int64_t div, int64_t mul, int64_t off) {
+    float scale, int64_t div, int64_t mul, int64_t off, u16* __restrict__ packed,
+    int mt) {
   const int lane = threadIdx.x & 63;
   const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
@@ -199,6 +200,8 @@ __global__ __launch_bounds__(256) void embed_kernel(
       v = pack8(f);
     }
     st16(dst + c, v);
+    // (decode, identity row map) the same 8 columns in the packed layout
+    if (packed) st16(packed + xoff((int)m, c, 0, mt), v);
   }
 }
 
@@ -389,7 +392,20 @@ int cadence_embed(const int32_t* tokens, const void* E, void* out,
   hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), tokens,
                      static_cast<const u16*>(E), static_cast<u16*>(out), ldo, M,
-                     (int)D, V, scale, row_div, row_mul, row_off);
+                     (int)D, V, scale, row_div, row_mul, row_off, nullptr, 0);
+  return (int)hipGetLastError();
+}
+
+int cadence_embed_packed(const int32_t* tokens, const void* E, void* out,
+                         int64_t ldo, void* packed, int64_t M, int64_t D,
+                         int64_t V, float scale, void* stream) {
+  if (D % 32 || ldo % 8 || M > 32 || !packed) return (int)hipErrorInvalidValue;
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), tokens,
+                     static_cast<const u16*>(E), static_cast<u16*>(out), ldo, M,
+                     (int)D, V, scale, M, (int64_t)0, (int64_t)0,
+                     static_cast<u16*>(packed), (int)((M + 15) / 16));
   return (int)hipGetLastError();
 }
 

@@ -311,6 +311,16 @@ int cadence_embed(const int32_t* tokens, const void* E, void* out,
                   int64_t row_div, int64_t row_mul, int64_t row_off,
                   void* stream);
 
+/* The decode step's embedding (M <= 32 rows, D % 32 == 0): as cadence_embed
+ * with the identity row map, and the same rows again in the decode
+ * activation layout (`packed`, D * 16 * ceil(M / 16) bf16): the first
+ * block's decode GEMVs apply its temporal_pre_norm on load from them, as
+ * every later block does from its predecessor's output (modules.py:994-1001
+ * and the block's RMSNorm, layers.py:60-78). */
+int cadence_embed_packed(const int32_t* tokens, const void* E, void* out,
+                         int64_t ldo, void* packed, int64_t M, int64_t D,
+                         int64_t V, float scale, void* stream);
+
 /* ---- recurrent block ----------------------------------------------------- */
 
 /* Conv1D, prefill (cache_in == NULL) or single-token decode (L == 1,
