@@ -70,6 +70,7 @@ _SIGS: dict[str, list] = {
     "cadence_layernorm": [P, I64, P, P, P, I64, I64, I64, F32, P],
     "cadence_embed": [P, P, P, I64, I64, I64, I64, F32, I64, I64, I64, P],
     "cadence_embed_packed": [P, P, P, I64, P, I64, I64, I64, F32, P],
+    "cadence_logits_argmax_tail": [P, I64, P, I64, I64, I64, I64, F32, P, P, I64, P, P],
     "cadence_conv1d": [P, I64, P, P, P, P, P, I64, P, I64, I64, I64, I64, I32,
                        P],
     "cadence_rnn_scan": [P, I64, P, I64, P, P, P, I64, P, I64, P, I64, I64, I64,
@@ -110,6 +111,15 @@ class CopyDesc(ctypes.Structure):
   """CadenceCopyDesc (cadence_kernels.h): one row-strided copy region."""
   _fields_ = [("src", P), ("dst", P), ("rows", I64), ("row_bytes", I64),
               ("src_stride", I64), ("dst_stride", I64)]
+
+
+class DecodeTail(ctypes.Structure):
+  """CadenceDecodeTail (cadence_kernels.h): the decode step's bookkeeping and
+  next-input rows for cadence_logits_argmax_tail."""
+  _fields_ = [("tokens_out", P), ("ld_out", I64), ("step", P), ("positions", P),
+              ("cur_out", P), ("done", P), ("eos_id", I32), ("pad_id", I32),
+              ("eos_from", I32), ("counter", P), ("embed", P), ("vocab", I64),
+              ("scale", F32), ("x_out", P), ("ldx_out", I64), ("packed_out", P)]
 
 
 class KernelLibraryMissing(RuntimeError):

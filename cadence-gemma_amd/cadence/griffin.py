@@ -199,6 +199,26 @@ class Griffin(nn.Module):
         float(self.config.logits_soft_cap or 0.0), return_logits)
     return nxt, (logits if return_logits else None), new_cache
 
+  @torch.no_grad()
+  def next_token_chained(self, x: torch.Tensor, xp: torch.Tensor,
+                         segment_pos: torch.Tensor, cache: Cache, tail: dict):
+    """One greedy decode step (T = 1, B <= 32) of a captured decode loop
+    whose input rows come from the previous step: `x` [B, D] / `xp` (packed)
+    hold the current token's embedding (Embedder.encode_packed), and the step
+    ends in one tail launch (ops.logits_argmax_tail) that does the argmax,
+    the decode_advance_ bookkeeping (tail: buf, step, pos, cur, done,
+    eos_args, counter) and writes the NEXT token's embedding back into x /
+    xp.  States update in place; returns next [B] int32."""
+    b, d = x.shape
+    pos = segment_pos.reshape(b, 1)
+    xn0 = ops.PackedRows(xp, b, d, self.blocks[0].temporal_pre_norm, x)
+    _, xn, _ = self.run_blocks(x, pos, b, 1, cache, True, True, final_norm=True,
+                               xn0=xn0)
+    return ops.logits_argmax_tail(
+        xn, self.embedder.input_embedding,
+        float(self.config.logits_soft_cap or 0.0),
+        dict(tail, x=x, xp=xp, scale=self.embedder.scale))
+
   def init_cache(self, batch_size: int, dtype: torch.dtype) -> Cache:
     dev = self.embedder.input_embedding.device
     cfg = self.config

@@ -467,6 +467,11 @@ class Embedder(nn.Module):
     ops.ops.embed_packed_(tok, self.input_embedding, self.scale, x, xp)
     return x, ops.PackedRows(xp, m, d, norm, x)
 
+  def encode_packed_into(self, tokens: torch.Tensor, x: torch.Tensor, xp: torch.Tensor):
+    """encode_packed into given buffers (a captured decode loop's rows)."""
+    tok = tokens.reshape(-1).to(torch.int32).contiguous()
+    ops.ops.embed_packed_(tok, self.input_embedding, self.scale, x, xp)
+
   def encode(self, x: torch.Tensor) -> torch.Tensor:
     out = torch.empty(x.numel(), self.embed_dim, dtype=self.input_embedding.dtype,
                       device=x.device)

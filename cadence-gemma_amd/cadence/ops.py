@@ -14,6 +14,7 @@ what the modules call; they route through `torch.ops.cadence`.
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import math
 import os
 from typing import NamedTuple
@@ -709,6 +710,46 @@ def _logits_argmax(x, embedding, soft_cap, return_logits, decode_layout=False,
   return logits, nxt
 
 
+@_reg("logits_argmax_tail_(Tensor x, Tensor embedding, float soft_cap, bool decode_layout, "
+      "int a_rows, Tensor(a!) tokens_out, Tensor(a!) step, Tensor(a!) positions, "
+      "Tensor(a!) cur, Tensor(a!)? done, int eos_id, int pad_id, int eos_from, "
+      "Tensor(a!) counter, Tensor table, float scale, Tensor(a!) x_out, "
+      "Tensor(a!) packed_out) -> Tensor")
+def _logits_argmax_tail(x, embedding, soft_cap, decode_layout, a_rows, tokens_out, step,
+                        positions, cur, done, eos_id, pad_id, eos_from, counter, table,
+                        scale, x_out, packed_out):
+  """The decode step's greedy tail (cadence_logits_argmax_tail): logits ->
+  argmax -> decode_advance bookkeeping -> the next step's input rows
+  (`table` = the row-major embedding)."""
+  D = embedding.shape[1]
+  if a_rows >= 0:
+    ldx, M = 0, a_rows
+  else:
+    ldx = _mat(x, "x")
+    M, D = x.shape
+  V = embedding.shape[0]
+  for t, name in ((tokens_out, "tokens_out"), (step, "step"), (positions, "positions"),
+                  (cur, "cur"), (counter, "counter")):
+    _need(t.dtype == _I32 and t.is_contiguous(), f"{name} int32")
+  _need(done is None or (done.dtype == _I32 and done.numel() == M + 1), "done int32[M + 1]")
+  _need(tokens_out.dim() == 2 and tokens_out.shape[0] == M, "tokens_out [M, steps]")
+  _need(tuple(x_out.shape) == (M, D) and want_packed(M, D) and
+        packed_out.numel() == D * 16 * (-(-M // 16)), "x_out / packed_out rows")
+  L = _lib.load()
+  nscr = L.cadence_logits_scratch_bytes(M, V, D)
+  scratch = torch.empty(nscr, dtype=torch.uint8, device=x.device)
+  nxt = torch.empty(M, dtype=_I32, device=x.device)
+  tail = _lib.DecodeTail(
+      _p(tokens_out), tokens_out.stride(0), _p(step), _p(positions), _p(cur),
+      _p(done) if done is not None else None, int(eos_id), int(pad_id), int(eos_from),
+      _p(counter), _p(table), table.shape[0], float(scale), _p(x_out), _mat(x_out, "x_out"),
+      _p(packed_out))
+  _lib.check(L.cadence_logits_argmax_tail(
+      _p(x), ldx, _p(embedding), 0 if decode_layout else D, M, V, D, float(soft_cap),
+      _p(nxt), _p(scratch), nscr, ctypes.byref(tail), _s(x)), "logits_argmax_tail")
+  return nxt
+
+
 @_reg("gemm_logits(Tensor x, Tensor embedding, float soft_cap, "
       "bool decode_layout=False, int a_rows=-1) -> Tensor")
 def _gemm_logits(x, embedding, soft_cap, decode_layout=False, a_rows=-1):
@@ -1328,6 +1369,19 @@ def logits_argmax(x2d, embedding, soft_cap, return_logits):
   if wd is not None:
     return ops.logits_argmax(a, wd, soft_cap, return_logits, True, ar)
   return ops.logits_argmax(a, embedding, soft_cap, return_logits, False, ar)
+
+
+def logits_argmax_tail(x2d, embedding, soft_cap, tail: dict):
+  """logits_argmax + decode_advance_ + embed_packed_ of the next token in one
+  tail launch (tail: the decode_advance_ operands and the next step's rows,
+  see Griffin.next_token_chained)."""
+  a, ar = _a(x2d)
+  wd = decode_weight(embedding) if x2d.shape[0] <= 32 else None
+  w, lay = (wd, True) if wd is not None else (embedding, False)
+  return ops.logits_argmax_tail_(
+      a, w, soft_cap, lay, ar, tail["buf"], tail["step"], tail["pos"], tail["cur"],
+      tail["done"], *tail["eos_args"], tail["counter"], embedding, tail["scale"],
+      tail["x"], tail["xp"])
 
 
 def gemm_logits(x2d, embedding, soft_cap):

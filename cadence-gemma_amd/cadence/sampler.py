@@ -481,6 +481,14 @@ class _DecodeGraph:
     self.step = torch.ones(1, dtype=torch.int32, device=device)
     self.done = (torch.zeros(batch + 1, dtype=torch.int32, device=device)
                  if eos_stop else None)
+    # the step's input rows, written by the previous replay's tail (the first
+    # replay's by `run`), and the tail's arrival counter
+    self.chained = ops.want_packed(batch, model.config.width)
+    if self.chained:
+      self.x = torch.zeros(batch, model.config.width, dtype=model.embedder.input_embedding.dtype,
+                           device=device)
+      self.xp = ops.packed_empty(batch, model.config.width, device).zero_()
+      self.counter = torch.zeros(1, dtype=torch.int32, device=device)
     self.cache = _clone_cache(cache_like)
     self.stream = torch.cuda.Stream(device=device)
     self.stream.wait_stream(torch.cuda.current_stream(device))
@@ -493,6 +501,14 @@ class _DecodeGraph:
     ops.claim_counters(self.stream, self)
 
   def _step(self):
+    if self.chained:
+      # embed -> blocks -> logits -> one tail launch (argmax, bookkeeping,
+      # the next step's embedding)
+      self.model.next_token_chained(
+          self.x, self.xp, self.pos, self.cache,
+          dict(buf=self.buf, step=self.step, pos=self.pos, cur=self.cur, done=self.done,
+               eos_args=self.eos_args, counter=self.counter))
+      return
     nxt, _, _ = self.model.next_token(self.cur[:, None], self.pos[:, None],
                                       self.cache, False, inplace=True)
     ops.ops.decode_advance_(nxt, self.buf, self.step, self.pos, self.cur,
@@ -525,6 +541,9 @@ class _DecodeGraph:
     if self.done is not None and done_in is not None:
       pairs.append((self.done, done_in))
     ops.copy_batched_(pairs)
+    if self.chained:
+      # the first replay's input rows (later replays' come from the tail)
+      self.model.embedder.encode_packed_into(self.cur, self.x, self.xp)
     self.step.fill_(start)
     if self.done is not None and done_in is None:
       self.done.zero_()

@@ -2489,6 +2489,95 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(
   }
 }
 
+// The decode step's tail (cadence_logits_argmax_tail): argmax_final_kernel's
+// reduction for row m, then decode_advance_kernel's bookkeeping for that row
+// and embed_kernel's gather of the token written, into the next replay's
+// input rows (row-major and packed).  *step is read by every workgroup before
+// it arrives on the counter; the last arrival advances it and ANDs the done
+// flags (written through to L2 before each arrival: the split-K hand-off of
+// gemm_stream_kernel, MI355X_MICROARCH.md "inter-workgroup visibility").
+__global__ __launch_bounds__(256) void argmax_tail_kernel(
+    const float* __restrict__ bval, const int* __restrict__ bidx, int nblk,
+    int32_t* __restrict__ next_out, CadenceDecodeTail a, int M, int D) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  __shared__ int tok;
+  const int m = blockIdx.x;
+  float v = -INFINITY;
+  int idx = 0x7fffffff;
+  constexpr int PER = 16;
+  for (int base = 0; base < nblk; base += 256 * PER) {
+    float ov[PER];
+    int oi[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int64_t i = (int64_t)m * nblk + min(base + u * 256 + (int)threadIdx.x, nblk - 1);
+      ov[u] = bval[i];
+      oi[u] = bidx[i];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u)
+      if (argmax_better(ov[u], oi[u], v, idx)) { v = ov[u]; idx = oi[u]; }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(v, off, 64);
+    const int oi = __shfl_xor(idx, off, 64);
+    if (argmax_better(ov, oi, v, idx)) { v = ov; idx = oi; }
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sv[wave] = v; si[wave] = idx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (argmax_better(sv[w], si[w], v, idx)) { v = sv[w]; idx = si[w]; }
+    next_out[m] = idx;
+    // decode_advance_kernel for row m
+    const int s = *a.step;
+    int32_t t = idx;
+    if (a.done) {
+      const int d = a.done[m];
+      if (d) t = a.pad_id;
+      __hip_atomic_store(a.done + m, d | (t == a.eos_id && s >= a.eos_from), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    a.tokens_out[(int64_t)m * a.ld_out + s] = t;
+    a.positions[m] += 1;
+    if (a.cur_out) a.cur_out[m] = t;
+    tok = t;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int n = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n == M - 1) {
+      int all = 1;
+      if (a.done) {
+        for (int b = 0; b < M; ++b)
+          all &= __hip_atomic_load(a.done + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.done[M] = all;
+      }
+      *a.step = s + 1;
+      __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  // embed_kernel for the token written (the next replay's input row)
+  const int64_t t = tok;
+  const u16* src = static_cast<const u16*>(a.embed) + (t >= 0 && t < a.vocab ? t : 0) * D;
+  u16* xo = static_cast<u16*>(a.x_out) + (int64_t)m * a.ldx_out;
+  u16* po = static_cast<u16*>(a.packed_out);
+  const int mt = (M + 15) / 16;
+  for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
+    uint4 w = ld16(src + c);
+    if (a.scale != 1.0f) {
+      float f[8];
+      unpack8(w, f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = bmul(f[i], a.scale);
+      w = pack8(f);
+    }
+    st16(xo + c, w);
+    st16(po + xoff(m, c, 0, mt), w);
+  }
+}
+
 constexpr int kSkinnyMaxM = 64;
 
 // Split-K finish of a residual GEMM that feeds an RMSNorm (decode): one
@@ -3496,6 +3585,40 @@ int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
   if (next_token)
     hipLaunchKernelGGL(argmax_final_kernel, dim3((unsigned)M), dim3(256), 0, st,
                        bval, bidx, (int)nblk, next_token);
+  return (int)hipGetLastError();
+}
+
+int cadence_logits_argmax_tail(const void* X, int64_t ldx, const void* E, int64_t lde,
+                               int64_t M, int64_t V, int64_t D, float soft_cap,
+                               int32_t* next_token, void* scratch, int64_t scratch_bytes,
+                               const CadenceDecodeTail* tail, void* stream) {
+  if (M <= 0) return 0;
+  if (!tail || !next_token || M > 32 || D % 32 || !tail->counter || !tail->step ||
+      !tail->positions || !tail->tokens_out || !tail->embed || !tail->x_out ||
+      !tail->packed_out || tail->ldx_out < D || tail->vocab <= 0)
+    return (int)hipErrorInvalidValue;
+  // the logits and the per-block (max, index) pairs, no argmax launch
+  const int rc = cadence_logits_argmax(X, ldx, E, lde, M, V, D, soft_cap, nullptr, nullptr,
+                                       scratch, scratch_bytes, stream);
+  if (rc != 0) return rc;
+  // where cadence_logits_argmax left the pairs
+  const int splits = skinny_splits(V, D, 1);
+  float* part = static_cast<float*>(scratch);
+  const float* bval;
+  const int* bidx;
+  int nb;
+  if (splits == 1) {
+    nb = (int)(V / 64);
+    bval = part;
+    bidx = reinterpret_cast<const int*>(part + M * nb);
+  } else {
+    nb = (int)((V + 255) / 256);
+    bval = part + (int64_t)splits * M * V;
+    bidx = reinterpret_cast<const int*>(bval + M * nb);
+  }
+  hipLaunchKernelGGL(argmax_tail_kernel, dim3((unsigned)M), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), bval, bidx, nb, next_token, *tail,
+                     (int)M, (int)D);
   return (int)hipGetLastError();
 }
 

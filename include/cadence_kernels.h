@@ -282,6 +282,38 @@ int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
                           void* scratch, int64_t scratch_bytes, void* stream);
 int64_t cadence_logits_scratch_bytes(int64_t M, int64_t V, int64_t D);
 
+/* The greedy decode step's tail in one launch after the logits: what
+ * cadence_logits_argmax's argmax, cadence_decode_advance and
+ * cadence_embed_packed do in three, for the captured decode step whose next
+ * replay starts from the rows this writes.  One workgroup per row m:
+ * next_token[m] = the argmax (as cadence_logits_argmax); the bookkeeping of
+ * cadence_decode_advance for row m (tokens_out, positions, cur_out, done[m]);
+ * then the embedding of the token written (E[t] * scale, an id outside [0,
+ * vocab) reads row 0) into x_out (row-major, ldx_out) and packed_out (the
+ * decode activation layout).  The last workgroup to arrive on `counter` (one
+ * int32, zero before the first launch; left zero) advances *step and sets
+ * done[M].  M <= 32, D % 32 == 0. */
+typedef struct CadenceDecodeTail {
+  int32_t* tokens_out;
+  int64_t ld_out;
+  int32_t* step;
+  int32_t* positions;
+  int32_t* cur_out;
+  int32_t* done;
+  int32_t eos_id, pad_id, eos_from;
+  int32_t* counter;
+  const void* embed;
+  int64_t vocab;
+  float scale;
+  void* x_out;
+  int64_t ldx_out;
+  void* packed_out;
+} CadenceDecodeTail;
+int cadence_logits_argmax_tail(const void* X, int64_t ldx, const void* E, int64_t lde,
+                               int64_t M, int64_t V, int64_t D, float soft_cap,
+                               int32_t* next_token, void* scratch, int64_t scratch_bytes,
+                               const CadenceDecodeTail* tail, void* stream);
+
 /* All-position logits (Griffin.forward with return_logits=True,
  * griffin.py:216-221): out[m, v] = softcap(bf16(x[m] . E[v])) (cap 0 = off).
  * Uses the GEMM workspace rules of cadence_gemm_linear. */
