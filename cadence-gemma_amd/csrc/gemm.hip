@@ -29,6 +29,7 @@
 #include <type_traits>
 #include <cstdio>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 #include "common.hpp"
 #include "../../include/cadence_kernels.h"
@@ -3588,6 +3589,12 @@ int cadence_logits_argmax(const void* X, int64_t ldx, const void* E,
   return (int)hipGetLastError();
 }
 
+// the descriptor's layout as the ctypes mirror declares it (cadence._lib.DecodeTail)
+static_assert(sizeof(CadenceDecodeTail) == 120 && offsetof(CadenceDecodeTail, counter) == 64 &&
+                  offsetof(CadenceDecodeTail, scale) == 88 &&
+                  offsetof(CadenceDecodeTail, packed_out) == 112,
+              "CadenceDecodeTail layout");
+
 int cadence_logits_argmax_tail(const void* X, int64_t ldx, const void* E, int64_t lde,
                                int64_t M, int64_t V, int64_t D, float soft_cap,
                                int32_t* next_token, void* scratch, int64_t scratch_bytes,
@@ -3601,7 +3608,7 @@ int cadence_logits_argmax_tail(const void* X, int64_t ldx, const void* E, int64_
   const int rc = cadence_logits_argmax(X, ldx, E, lde, M, V, D, soft_cap, nullptr, nullptr,
                                        scratch, scratch_bytes, stream);
   if (rc != 0) return rc;
-  // where cadence_logits_argmax left the pairs
+  // where cadence_logits_argmax left the pairs (its scratch layout)
   const int splits = skinny_splits(V, D, 1);
   float* part = static_cast<float*>(scratch);
   const float* bval;

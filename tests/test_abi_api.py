@@ -168,6 +168,15 @@ def test_positions_and_sampler_prompt_layout():
   assert pos.tolist() == [[-1, -1, 0, 1, 2], [0, 1, 2, 3, 4]]
 
 
+def test_decode_tail_descriptor_layout():
+  """cadence._lib.DecodeTail mirrors CadenceDecodeTail (the C side
+  static_asserts the same size and offsets)."""
+  import ctypes
+  T = _lib.DecodeTail
+  assert ctypes.sizeof(T) == 120
+  assert T.counter.offset == 64 and T.scale.offset == 88 and T.packed_out.offset == 112
+
+
 def test_prefill_gemm_plan_host_arithmetic():
   """The prefill engine's tile height and K-split plan (host-only; 256 CUs
   assumed when no GPU is visible): bench shapes keep one pass with the tile
