@@ -1,6 +1,8 @@
 // LAB (round 6): where the gated GEMM's time goes -- gemm_w4_kernel (csrc/gemm.hip)
 // copied at round 6 (commit of this file) with switches: 1 no per-K-tile vmcnt(0),
-// 2 no per-K-tile barrier, 4 no epilogue, 8 no in-loop DMA, 16 no MFMA.
+// 2 no per-K-tile barrier, 4 no epilogue, 8 no in-loop DMA, 16 no MFMA;
+// 32 / 64: all / half of a K-tile's DMA issued ahead of the segment's MFMAs
+// (correct results: schedule variants).
 // Results are wrong for every switch but 0: timing only.  Not product code.
 #include "../cadence-gemma_amd/csrc/gemm.hip"
 
@@ -83,6 +85,24 @@ __global__ __launch_bounds__(256, 1) void w4_lab_kernel(
     const bool live = dtile < nk;
     const char* bk = live ? reinterpret_cast<const char*>(base + dtile * BK) : zpage;
     int nr = 0, nd = 0;
+    if constexpr ((LAB & 32) != 0) {
+      // lab: the K-tile's 16 DMA pieces issued ahead of the segment's MFMAs
+      if (dma_on) {
+#pragma unroll
+        for (; nd < 16; ++nd)
+          __builtin_amdgcn_global_load_lds((gptr_t)(bk + (live ? soff[nd] : zoff)),
+                                           (lptr_t)(dst + nd * 64), 16, 0, 0);
+      }
+    }
+    if constexpr ((LAB & 64) != 0) {
+      // lab: the first 8 pieces ahead, the rest interleaved
+      if (dma_on) {
+#pragma unroll
+        for (; nd < 8; ++nd)
+          __builtin_amdgcn_global_load_lds((gptr_t)(bk + (live ? soff[nd] : zoff)),
+                                           (lptr_t)(dst + nd * 64), 16, 0, 0);
+      }
+    }
 #pragma unroll
     for (int n = 0; n < MR * 8; ++n) {
       const int i = n / 8, j = n % 8;
@@ -185,6 +205,7 @@ extern "C" int w4_lab(const void* A, const void* W, const void* bg, const void* 
                            a, K, w, K, (int)M, (int)N, (int)K, (int64_t)0, (int64_t)0, epi); break;
   switch (lab) {
     W4L(0) W4L(1) W4L(2) W4L(3) W4L(4) W4L(8) W4L(9) W4L(16) W4L(20) W4L(24) W4L(28)
+    W4L(32) W4L(64)
     default: return -1;
   }
 #undef W4L
