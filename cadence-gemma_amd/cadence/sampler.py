@@ -463,7 +463,9 @@ class _DecodeGraph:
 
   Static buffers: current token, positions, token buffer, step counter, the
   EOS flags and a private copy of every block cache (recurrent states and
-  attention ring buffers are updated in place by the kernels).  `run`
+  attention ring buffers are updated in place by the kernels); for B <= 32
+  also the step's input rows (row-major and packed), which each replay's
+  tail launch fills for the next one, and that launch's arrival counter.  `run`
   copies the prefill state in, replays the graph, and copies the generated
   tokens out, all on the caller's current stream.  Capture happens on a
   private stream (hipGraph capture cannot use the null stream), which also
@@ -502,8 +504,9 @@ class _DecodeGraph:
 
   def _step(self):
     if self.chained:
-      # embed -> blocks -> logits -> one tail launch (argmax, bookkeeping,
-      # the next step's embedding)
+      # (input rows already embedded) blocks -> logits -> one tail launch:
+      # argmax, bookkeeping, the next step's embedding
+      # (Griffin.next_token_chained)
       self.model.next_token_chained(
           self.x, self.xp, self.pos, self.cache,
           dict(buf=self.buf, step=self.step, pos=self.pos, cur=self.cur, done=self.done,
