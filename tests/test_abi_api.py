@@ -1,5 +1,6 @@
 """C-ABI library + Python API surface (CPU only; no compute calls)."""
 
+import ctypes
 import os
 import re
 
@@ -50,6 +51,29 @@ def test_host_contract_checks_without_gpu():
   # contract violations are rejected before any launch (N % 64 != 0)
   assert lib.cadence_gemm_linear(None, 0, None, 0, None, None, 0, None, 0, 8,
                                  100, 64, 0, 8, 0, 0, None, 0, None) != 0
+
+
+def test_decode_step_entry_points_reject_bad_shapes_without_gpu():
+  """cadence_embed_packed / cadence_logits_argmax_tail (ABI 17) check their
+  contract on the host before any launch."""
+  lib = _lib.load()
+  # 33 rows (> 32), D not a multiple of 32, no packed buffer
+  assert lib.cadence_embed_packed(None, None, None, 2560, 8, 33, 2560, 256000, 1.0, None) != 0
+  assert lib.cadence_embed_packed(None, None, None, 2568, 8, 32, 2568, 256000, 1.0, None) != 0
+  assert lib.cadence_embed_packed(None, None, None, 2560, None, 32, 2560, 256000, 1.0,
+                                  None) != 0
+  assert lib.cadence_embed_packed(None, None, None, 2560, 8, 0, 2560, 256000, 1.0, None) == 0
+  # no descriptor, no next-token buffer, 33 rows
+  assert lib.cadence_logits_argmax_tail(None, 0, None, 0, 32, 256000, 2560, 30.0, 8, None, 0,
+                                        None, None) != 0
+  t = _lib.DecodeTail()
+  assert lib.cadence_logits_argmax_tail(None, 0, None, 0, 33, 256000, 2560, 30.0, 8, None, 0,
+                                        ctypes.byref(t), None) != 0
+  # a descriptor without its counter / rows
+  assert lib.cadence_logits_argmax_tail(None, 0, None, 0, 32, 256000, 2560, 30.0, 8, None, 0,
+                                        ctypes.byref(t), None) != 0
+  assert lib.cadence_logits_argmax_tail(None, 0, None, 0, 0, 256000, 2560, 30.0, None, None,
+                                        0, None, None) == 0
 
 
 def test_reference_exports_present():
