@@ -190,6 +190,23 @@ __global__ __launch_bounds__(256, 1) void w4_lab_kernel(
 }
 
 
+// epilogue variants (results wrong, timing only): V & 1 the gate x up math
+// replaced by one add per pair, V & 2 no global stores (the LDS staging kept)
+template <int V>
+struct EpiGatedLab : EpiGatedGelu {
+  CADENCE_DEV uint32_t out2(f32x2 g, f32x2 u, float bg, float bu) const {
+    if constexpr ((V & 1) != 0) return pk2bf(f32x2{g.x + u.x, g.y + u.y});
+    else return EpiGatedGelu::out2(g, u, bg, bu);
+  }
+  CADENCE_DEV void store8(int64_t m, int f, uint4 v) const {
+    if constexpr ((V & 2) != 0) {
+      if (v.x == 0x12345678u) out[0] = 1;
+    } else {
+      EpiGatedGelu::store8(m, f, v);
+    }
+  }
+};
+
 }  // namespace
 
 extern "C" int w4_lab(const void* A, const void* W, const void* bg, const void* bu, void* out,
@@ -206,6 +223,11 @@ extern "C" int w4_lab(const void* A, const void* W, const void* bg, const void* 
   switch (lab) {
     W4L(0) W4L(1) W4L(2) W4L(3) W4L(4) W4L(8) W4L(9) W4L(16) W4L(20) W4L(24) W4L(28)
     W4L(32) W4L(64)
+#define W4E(L_, V_) case L_: hipLaunchKernelGGL((w4_lab_kernel<EpiGatedLab<V_>, 8, 0>), grid, dim3(256), 0, \
+                           st, a, K, w, K, (int)M, (int)N, (int)K, (int64_t)0, (int64_t)0, \
+                           EpiGatedLab<V_>{epi}); break;
+    W4E(101, 1) W4E(102, 2) W4E(103, 3)
+#undef W4E
     default: return -1;
   }
 #undef W4L

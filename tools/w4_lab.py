@@ -14,7 +14,8 @@ LABS = {0: "product", 1: "no vmcnt(0) per K-tile", 2: "no barrier per K-tile",
         3: "neither", 4: "no epilogue", 8: "no in-loop DMA", 9: "no DMA, no vmcnt",
         16: "no MFMA", 20: "no MFMA, no epilogue", 24: "no MFMA, no DMA",
         28: "no MFMA, DMA, epilogue", 32: "DMA issued ahead (all)",
-        64: "DMA issued ahead (half)"}
+        64: "DMA issued ahead (half)", 101: "epilogue: one add for the math",
+        102: "epilogue: no global stores", 103: "epilogue: neither"}
 
 
 def main():
