@@ -7,6 +7,35 @@
 #include "../cadence-gemma_amd/csrc/gemm.hip"
 
 namespace {
+// lab epilogue (LAB & 128): the gated outputs stored straight from the
+// accumulator layout, no LDS staging -- two 2-B stores per pair of rows
+// (16 lanes = 32 contiguous bytes of one row per store instruction)
+template <class Epi, int MR>
+CADENCE_DEV void direct_gated_epilogue(const Epi& epi, f32x4 (&acc)[MR][4], int mbase,
+                                       int nbase, int lane, int M, int g) {
+  const int rsub = (lane >> 4) * 4, csub = lane & 15;
+  const int obase = nbase / 2;
+  float bgv[2], buv[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bgv[h] = epi.bias_at(false, obase + h * 16 + csub, g);
+    buv[h] = epi.bias_at(true, obase + h * 16 + csub, g);
+  }
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const uint32_t w = epi.out2(f32x2{acc[i][h][r], acc[i][h][r + 1]},
+                                    f32x2{acc[i][2 + h][r], acc[i][2 + h][r + 1]}, bgv[h],
+                                    buv[h]);
+        const int row = mbase + i * 16 + rsub + r, c = obase + h * 16 + csub;
+        if (row < M) epi.out[(int64_t)row * epi.ldo + c] = (u16)w;
+        if (row + 1 < M) epi.out[(int64_t)(row + 1) * epi.ldo + c] = (u16)(w >> 16);
+      }
+}
+
 template <class Epi, int MR, int LAB>
 __global__ __launch_bounds__(256, 1) void w4_lab_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ W,
@@ -181,7 +210,9 @@ __global__ __launch_bounds__(256, 1) void w4_lab_kernel(
       for (int i = 0; i < MR; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) half[i][j] = acc[i][h * 4 + j];
-      if constexpr (!(LAB & 4))
+      if constexpr ((LAB & 128) != 0)
+        direct_gated_epilogue<Epi, MR>(epi, half, mbase, nbase, lane, M, g);
+      else if constexpr (!(LAB & 4))
         big_epilogue<Epi, MR>(epi, half, st + h * (128 * 64), mbase, nbase, lane, M, N, g);
       else if (acc[0][0][0] == 12345.0f)   // keep the accumulators live
         epi.out[0] = 1;
@@ -222,7 +253,7 @@ extern "C" int w4_lab(const void* A, const void* W, const void* bg, const void* 
                            a, K, w, K, (int)M, (int)N, (int)K, (int64_t)0, (int64_t)0, epi); break;
   switch (lab) {
     W4L(0) W4L(1) W4L(2) W4L(3) W4L(4) W4L(8) W4L(9) W4L(16) W4L(20) W4L(24) W4L(28)
-    W4L(32) W4L(64)
+    W4L(32) W4L(64) W4L(128)
 #define W4E(L_, V_) case L_: hipLaunchKernelGGL((w4_lab_kernel<EpiGatedLab<V_>, 8, 0>), grid, dim3(256), 0, \
                            st, a, K, w, K, (int)M, (int)N, (int)K, (int64_t)0, (int64_t)0, \
                            EpiGatedLab<V_>{epi}); break;

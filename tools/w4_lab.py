@@ -15,7 +15,8 @@ LABS = {0: "product", 1: "no vmcnt(0) per K-tile", 2: "no barrier per K-tile",
         16: "no MFMA", 20: "no MFMA, no epilogue", 24: "no MFMA, no DMA",
         28: "no MFMA, DMA, epilogue", 32: "DMA issued ahead (all)",
         64: "DMA issued ahead (half)", 101: "epilogue: one add for the math",
-        102: "epilogue: no global stores", 103: "epilogue: neither"}
+        102: "epilogue: no global stores", 103: "epilogue: neither",
+        128: "epilogue: direct 2-B stores, no LDS"}
 
 
 def main():
@@ -34,6 +35,15 @@ def main():
   bu = torch.zeros(F, device=dev, dtype=torch.bfloat16)
   out = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
   flops = 2.0 * M * 2 * F * K
+  outs = {}
+  for lab in (0, 128):
+    out.zero_()
+    assert lib.w4_lab(a.data_ptr(), w.data_ptr(), bg.data_ptr(), bu.data_ptr(), out.data_ptr(),
+                      M, F, K, lab, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    outs[lab] = out.clone()
+  print("direct-store epilogue bitwise equal to the staged one:",
+        torch.equal(outs[0], outs[128]), flush=True)
   times = {k: [] for k in LABS}
   for _ in range(rounds):
     for lab in LABS:
