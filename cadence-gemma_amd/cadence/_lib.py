@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # CADENCE_LIB_PATH: the host-ASan build of the same C-ABI
 # (tools/asan_host.sh, CPU-only contract tests); unset everywhere else
 LIB_PATH = os.environ.get("CADENCE_LIB_PATH") or os.path.join(_HERE, "libcadence_hip.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -57,6 +57,9 @@ _SIGS: dict[str, list] = {
                                           I64, I64, I64, P, I64, P, P],
     "cadence_gemm_linear_rmsnorm": [P, I64, P, I64, P, P, I64, P, I64, I64, I64,
                                     I64, P, F32, P, I64, P, I64, P],
+    "cadence_recurrent_decode_front_plan": [I64, I64, I64, I64, I64],
+    "cadence_recurrent_decode_front": [P, P, P, P, I64, I64, I64, P, P, P, I32, F32, P, P,
+                                       P, P, P, P, P, I64, I64, P, P, P],
     "cadence_rglru_step": [P, I64, P, I64, P, P, P, P, P, P, I64, P, I64, I64,
                            I64, I64, P, I64, P],
     "cadence_gemm_vit_residual": [P, I64, P, I64, P, P, P, I64, I64, I64, I64,

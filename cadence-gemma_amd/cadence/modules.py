@@ -254,10 +254,14 @@ class RecurrentBlock(nn.Module):
         cache.conv1d_state.dtype == xn2d.dtype):
       # decode: the y|x projection runs the x branch's Conv1D step in its
       # epilogue; conv / RG-LRU states are advanced in place by the kernels
-      yc = ops.linear_conv1d_(xn2d, w, bias, self.conv_1d.w, self.conv_1d.b,
-                              cache.conv1d_state)       # [M, 2E]: y | conv(x)
-      gated = self.rg_lru.step_(yc[:, e:], pos.view(-1), cache.rg_lru_state,
-                                yc[:, :e], packed_out=True)
+      gated = ops.recurrent_decode_front_(
+          xn2d, w, bias, self.conv_1d.w, self.conv_1d.b, cache.conv1d_state,
+          self.rg_lru.packed(), pos.view(-1), cache.rg_lru_state)
+      if gated is None:   # rows / shapes outside the one-launch plan
+        yc = ops.linear_conv1d_(xn2d, w, bias, self.conv_1d.w, self.conv_1d.b,
+                                cache.conv1d_state)     # [M, 2E]: y | conv(x)
+        gated = self.rg_lru.step_(yc[:, e:], pos.view(-1), cache.rg_lru_state,
+                                  yc[:, :e], packed_out=True)
       out, hn = _out_proj(gated, self.linear_out, resid2d, norm, lazy)
       return out, hn, cache
     yx = ops.linear(xn2d, w, bias)                       # [M, 2E]: y | x

@@ -185,6 +185,22 @@ def _counters(dev: torch.device, n: int):
   return buf
 
 
+_WAIT_ERR: dict[int, torch.Tensor] = {}
+
+
+def wait_err(dev: torch.device):
+  """int32 flag a launch with an inter-workgroup wait sets to 1 if a wait
+  gave up (never expected; tests read it), one per device.  None while
+  capturing before first use."""
+  idx = dev.index if dev.index is not None else torch.cuda.current_device()
+  buf = _WAIT_ERR.get(idx)
+  if buf is None:
+    if torch.cuda.is_current_stream_capturing():
+      return None
+    buf = _WAIT_ERR[idx] = torch.zeros(1, dtype=torch.int32, device=dev)
+  return buf
+
+
 def _copy_region(dst: torch.Tensor, src: torch.Tensor):
   """(rows, row_bytes, src_stride, dst_stride) of a dst <- src copy whose
   views are each [rows, contiguous rest] (a whole contiguous tensor is one
@@ -443,6 +459,47 @@ def _gemm_linear_conv1d(a, w, bias, conv_w, conv_b, conv_state, w_packed=False,
       _norm_flag(norm, lda), float(norm_eps), _s(a)),
       "gemm_linear_conv1d")
   return out
+
+
+@_reg("recurrent_decode_front(Tensor a, int a_rows, Tensor w, Tensor? bias, "
+      "Tensor conv_w, Tensor conv_b, Tensor(a!) conv_state, Tensor wg, "
+      "Tensor bias_x, Tensor bias_a, Tensor softplus_a, Tensor segment_pos, "
+      "Tensor(b!) h, Tensor(c!) counters, Tensor(d!) err, bool norm=False, "
+      "float norm_eps=0.0) -> (Tensor, Tensor)")
+def _recurrent_decode_front(a, a_rows, w, bias, conv_w, conv_b, conv_state, wg, bias_x,
+                            bias_a, softplus_a, segment_pos, h, counters, err, norm=False,
+                            norm_eps=0.0):
+  """Decode recurrent-block front in one launch: gemm_linear_conv1d_ (packed
+  rows, decode-packed w) then rglru_step_ on its output (gate = y branch,
+  decode-packed wg, packed y).  Returns (yx [M, 2E], y packed rows);
+  conv_state and h advance in place."""
+  M = a_rows
+  N, K = w.shape[0], w.shape[1]
+  TW, E = conv_w.shape
+  H, two_bw, bw = wg.shape
+  _need(TW == 4 and N == 2 * E and conv_b.numel() == E, "conv width vs projection width")
+  _need(two_bw == 2 * bw and H * bw == E, "gate weight shape")
+  _need(a.numel() == K * 16 * (-(-M // 16)), "a: packed rows size")
+  _need(conv_state.is_contiguous() and conv_state.dtype == _BF16 and
+        tuple(conv_state.shape) == (M, TW - 1, E), "conv state")
+  _need(h.dtype == _F32 and h.is_contiguous() and tuple(h.shape) == (M, E),
+        "h: [M, E] fp32 contiguous")
+  _need(segment_pos.dtype == _I32 and segment_pos.numel() == M, "segment_pos")
+  _need(counters.dtype == _I32 and counters.numel() >= 2 * H and
+        err.dtype == _I32 and err.numel() >= 1, "counters / err")
+  if bias is not None:
+    _need(bias.numel() == N and bias.dtype == _BF16, "bias shape/dtype")
+  lib = _lib.load()
+  _need(lib.cadence_recurrent_decode_front_plan(M, E, K, H, bw) == 1,
+        "recurrent_decode_front: shape outside its plan")
+  yx = torch.empty(M, N, dtype=_BF16, device=a.device)
+  y = packed_empty(M, E, a.device)
+  _lib.check(lib.cadence_recurrent_decode_front(
+      _p(a), _p(w), _p(bias), _p(yx), M, E, K, _p(conv_w.contiguous()),
+      _p(conv_b.contiguous()), _p(conv_state), 1 if norm else 0, float(norm_eps),
+      _p(wg), _p(bias_x), _p(bias_a), _p(softplus_a), _p(segment_pos.contiguous()),
+      _p(h), _p(y), H, bw, _p(counters), _p(err), _s(a)), "recurrent_decode_front")
+  return yx, y
 
 
 @_reg("gemm_linear_rmsnorm(Tensor a, Tensor w, Tensor? bias, Tensor? resid, "
@@ -1303,6 +1360,37 @@ def linear_conv1d_(x2d, w, bias, conv_w, conv_b, conv_state):
                                    nm is not None,
                                    float(nm.eps) if nm is not None else 0.0)
   return ops.gemm_linear_conv1d_(a, w, bias, conv_w, conv_b, conv_state, False, ar)
+
+
+FRONT_ONE_LAUNCH = False  # True: the one-launch front where it fits (A/B: tools/front_ab.py)
+
+
+def recurrent_decode_front_(x2d, w, bias, conv_w, conv_b, conv_state, gates, pos_flat, h):
+  """The decode recurrent-block front (y|x projection + Conv1D step + RG-LRU
+  gates + scan step, gate = y) as one launch when the rows and shapes fit
+  its plan: PackedRows y, conv_state / h advanced in place.  None otherwise
+  (the caller runs linear_conv1d_ + rglru_step_)."""
+  if not FRONT_ONE_LAUNCH:
+    return None
+  M, E = x2d.shape[0], conv_w.shape[1]
+  wgt, bx, ba, sp = gates
+  H, _, bw = wgt.shape
+  if not (isinstance(x2d, PackedRows) and x2d.data.is_cuda and conv_w.shape[0] == 4 and
+          _lib.load().cadence_recurrent_decode_front_plan(M, E, w.shape[1], H, bw)):
+    return None
+  wg = decode_weight(wgt)
+  if wg is None:
+    return None
+  a, ar, wd, nm = _an(x2d, w)
+  if wd is None:
+    return None
+  cnt, err = _counters(x2d.device, 2 * H), wait_err(x2d.device)
+  if cnt is None or err is None:
+    return None
+  _, y = ops.recurrent_decode_front(a, ar, wd, bias, conv_w, conv_b, conv_state, wg, bx, ba,
+                                    sp, pos_flat, h, cnt, err, nm is not None,
+                                    float(nm.eps) if nm is not None else 0.0)
+  return PackedRows(y, M, E)
 
 
 def linear_rmsnorm(x2d, w, bias, resid, norm, packed_out=None, lazy=False):

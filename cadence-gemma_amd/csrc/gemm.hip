@@ -663,6 +663,229 @@ struct EpiRglruGates {
   }
 };
 
+// Decode recurrent-block front in ONE launch (verdict r05 item 3): the y|x
+// projection + Conv1D step (EpiLinearConv), then, in the same workgroups,
+// the RG-LRU gate GEMV + scan step of EpiRglruGates (layers.py:345-365,
+// :175-182) -- no second launch.  Each head's 2 bw / 32 gate items (the
+// paired 16-channel blocks of gemm_stream_kernel<32, 1, 1, EpiRglruGates>)
+// are taken one each by the head's 2 bw / 32 y|x workgroups (its y-branch
+// and x-branch column pairs), after all of them have published their
+// outputs: y|x outputs are stored write-through (sc1), each workgroup
+// drains its stores, arrives on the head's counter and polls it (one lane,
+// s_sleep) until every workgroup of the head has arrived, then reads the
+// conv outputs and the y gate with sc1 loads (MI355X_MICROARCH.md
+// "inter-workgroup visibility", first protocol row; the y|x grid is one
+// round, so the awaited workgroups are running or about to be).  The gate
+// weights and the epilogue's other operands are loaded before the wait.
+// Same fragments, k order, reduction order and epilogue as the two
+// launches: bitwise equal (tests/test_recurrent_front_gpu.py).  Counters:
+// cnt[head] counts arrivals, cnt[heads + head] departures; the head's last
+// workgroup to depart zeroes both (every workgroup departs only after its
+// own wait saw all arrivals), so the buffer is left as it was found.
+template <class E, class = void>
+struct EpiPost { static constexpr bool value = false; };
+template <class E>
+struct EpiPost<E, std::void_t<decltype(E::kPost)>> {
+  static constexpr bool value = E::kPost;
+};
+
+// write-through (sc1) accesses of the hand-off: 16-B buffer stores / loads
+// with aux = sc1, 4-B agent-scope relaxed loads (global_load_dword sc1)
+CADENCE_DEV __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+// element i of a bf16 array through `r` (its base): the aligned dword that
+// holds it, loaded sc1 (buffer_load_dword), then its half
+CADENCE_DEV float ld_sc1_bf(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  const uint32_t w = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)((i & ~(int64_t)1) * 2), 0, 16);
+  return bf2f((i & 1) ? (u16)(w >> 16) : (u16)(w & 0xffff));
+}
+
+template <int TW>
+struct EpiLinearConvGates : EpiLinearConv<TW> {
+  static constexpr bool kPost = true;
+  EpiRglruGates ge;     // x = out + conv_lo (ldx = ldo), gate = out (ldg = ldo), packed y
+  const u16* wg;        // decode-packed gate weights [H][2 bw / 16][bw / 32][64][8]
+  int32_t* cnt;         // [2 H] arrive / depart counters, zero before and after
+  int32_t* err;         // set to 1 if an arrival wait gave up (never expected)
+  using Pref = typename EpiLinearConv<TW>::Pref;
+  // this workgroup's [32 rows][32 columns] of `out`, staged so that the
+  // hand-off leaves in 16-B write-through stores (post, step 1)
+  CADENCE_DEV static u16* stage() {
+    __shared__ __attribute__((aligned(16))) u16 buf[32 * 32];
+    return buf;
+  }
+  CADENCE_DEV void put(int64_t m, int n, u16 v) const {
+    stage()[m * 32 + (n & 31)] = v;
+  }
+  // EpiLinearConv::apply_pf with `out` staged in LDS
+  CADENCE_DEV void apply_pf(int64_t m, int n, float v, int g, const Pref& p) const {
+    const float x = this->value(m, n, v, g);
+    if (n < this->conv_lo) {
+      put(m, n, f2bf(x));
+      return;
+    }
+    float acc = bmul(x, bf2f(p.w[TW - 1]));
+#pragma unroll
+    for (int s = 1; s < TW; ++s)
+      acc = badd(acc, bmul(bf2f(p.s[TW - 1 - s]), bf2f(p.w[TW - 1 - s])));
+    acc = badd(acc, bf2f(p.b));
+    put(m, n, f2bf(acc));
+    u16* srow = this->state + m * (int64_t)(TW - 1) * this->E + (n - this->conv_lo);
+#pragma unroll
+    for (int r = 0; r + 1 < TW - 1; ++r) srow[(int64_t)r * this->E] = p.s[r + 1];
+    if constexpr (TW > 1) srow[(int64_t)(TW - 2) * this->E] = f2bf(x);
+  }
+  CADENCE_DEV void apply(int64_t m, int n, float v, int g) const {
+    apply_pf(m, n, v, g, this->prefetch(m, n));
+  }
+  // the gate item of this workgroup; `red` = the stream kernel's 8 x 1024
+  // float reduction buffer (idle again), M <= 32 rows
+  // this workgroup's gate item: head, rank among the head's 2 bw / 32
+  // workgroups, the two packed gate-weight column blocks, the channel of
+  // thread t (its row is t / 16)
+  struct Item { int head, per, colg[2], e; };
+  CADENCE_DEV Item item() const {
+    const int bw = ge.bw, El = this->conv_lo;
+    const int col0 = blockIdx.x * 32;                       // this workgroup's y|x columns
+    const bool xb = col0 >= El;
+    const int c0 = xb ? col0 - El : col0;
+    Item it;
+    it.head = c0 / bw;
+    const int rank = (c0 % bw) / 32 + (xb ? bw / 32 : 0);
+    it.per = 2 * bw / 32;
+    const int grp = rank >> 1, half = rank & 1;
+    it.colg[0] = grp * 64 + half * 16;
+    it.colg[1] = grp * 64 + 32 + half * 16;
+    it.e = it.head * bw + grp * 32 + half * 16 + (threadIdx.x & 15);
+    return it;
+  }
+  // operands of the gate stage that do not depend on this launch (gate
+  // weights: k-step = wave, K = bw; bias / softplus / position / state),
+  // loaded at kernel start, ahead of the y|x stream
+  struct PostPref { uint4 wb[2]; u16 bx, ba, sp; int reset; float h; };
+  CADENCE_DEV PostPref pre(int M) const {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, bw = ge.bw;
+    const Item it = item();
+    const int k = wave * 32;
+    const u16* zpage = reinterpret_cast<const u16*>(kZeroPage + lane);
+    const u16* W = wg + (int64_t)it.head * 2 * bw * bw;
+    PostPref p;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      p.wb[j] = ld16_nt(k < bw ? W + (((int64_t)(it.colg[j] >> 4) * (bw >> 5) + (k >> 5)) * 64 +
+                                      lane) * 8
+                               : zpage);
+    const int pm = min((int)(threadIdx.x >> 4), M - 1);
+    p.bx = ge.bias_x[it.e];
+    p.ba = ge.bias_a[it.e];
+    p.sp = ge.softplus_a[it.e];
+    p.reset = ge.segpos[pm] == 0;
+    p.h = ge.h[(int64_t)pm * ge.ldh + it.e];
+    return p;
+  }
+  // the gate item of this workgroup; `red` = the stream kernel's 8 x 1024
+  // float reduction buffer (idle again), M <= 32 rows
+  CADENCE_DEV void post(float* red, int M, const PostPref& pp) const {
+    constexpr int MS = 32, MR = 2, NREP = 2, S = MS * 16 * NREP;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int bw = ge.bw, heads = this->conv_lo / bw;
+    const int col0 = blockIdx.x * 32;
+    const Item it = item();
+    const int head = it.head, per = it.per, e = it.e;
+    // 1. this workgroup's y|x outputs leave write-through (16-B sc1 stores:
+    //    4 per row), are out of its queue, then the workgroup arrives
+    __syncthreads();
+    if (tid < M * 4) {
+      const int r = tid >> 2, q = tid & 3;
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = *reinterpret_cast<const u32x4*>(stage() + r * 32 + q * 8);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          v, rsrc_of(this->out), (int)(((int64_t)r * this->ldo + col0 + q * 8) * 2), 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_fetch_add(cnt + head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int K = bw;
+    const int k = wave * 32, koff = 8 * (lane >> 4);
+    const bool ok = k < K;
+    const int pm = min(tid >> 4, M - 1);
+    const uint4* wb = pp.wb;
+    const u16 pbx = pp.bx, pba = pp.ba, psp = pp.sp;
+    const int preset = pp.reset;
+    const float ph = pp.h;
+    // 3. every workgroup of the head has published
+    if (tid == 0) {
+      int n = 0;
+      while (__hip_atomic_load(cnt + head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < per) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++n == (1 << 24)) {   // give up rather than hang the queue (never expected)
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    // 4. the conv outputs (A operand) and this thread's x / gate values, sc1
+    const __amdgpu_buffer_rsrc_t xr = rsrc_of(ge.x);
+    uint4 xa[MR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int m = i * 16 + (lane & 15);
+      const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+          xr, (int)(((int64_t)min(m, M - 1) * ge.ldx + head * bw + k + koff) * 2), 0, 16));
+      xa[i] = (ok && m < M) ? v : make_uint4(0, 0, 0, 0);
+    }
+    const float pxv = ld_sc1_bf(xr, (int64_t)pm * ge.ldx + e);
+    const float pgt = ld_sc1_bf(rsrc_of(ge.gate), (int64_t)pm * ge.ldg + e);
+    f32x4 acc[MR][NREP];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NREP; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8, xa[i]), __builtin_bit_cast(bf16x8, wb[j]),
+            f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    const int rsub = (lane >> 4) * 4, csub = lane & 15;
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NREP; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          red[wave * S + ((i * 16 + rsub + r) * NREP + j) * 16 + csub] = acc[i][j][r];
+    __syncthreads();
+    // 5. fixed-order reduction and the paired epilogue (EpiRglruGates::apply2_pf)
+    const int m = tid >> 4, c = tid & 15;
+    if (m < M) {
+      float v[NREP];
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        const float* rr = red + (m * NREP + j) * 16 + c;
+        v[j] = ((rr[0] + rr[S]) + (rr[2 * S] + rr[3 * S])) +
+               ((rr[4 * S] + rr[5 * S]) + (rr[6 * S] + rr[7 * S]));
+      }
+      float av, nx;
+      ge.chain(badd(rbf(v[0]), bf2f(pbx)), badd(rbf(v[NREP - 1]), bf2f(pba)), pxv, bf2f(psp),
+               preset != 0, av, nx);
+      const float hn = add_rn(mul_rn(av, ph), nx);
+      ge.h[(int64_t)m * ge.ldh + e] = hn;
+      ge.y_out[xoff(m, e, ge.ldy, ge.mt)] = f2bf(bmul(rbf(hn), pgt));
+    }
+    // 6. depart; the head's last workgroup to depart zeroes both counters
+    if (tid == 0) {
+      const int d = __hip_atomic_fetch_add(cnt + heads + head, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      if (d == per - 1) {
+        __hip_atomic_store(cnt + head, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt + heads + head, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+};
+template <int TW> struct EpiNormIn<EpiLinearConvGates<TW>> { static constexpr bool value = true; };
+
 struct EpiVitResid {
   static constexpr bool kPaired = false;
   static constexpr bool kStaged = false;
@@ -1511,6 +1734,11 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
       for (int j = 0; j < NREP; ++j) pf[j] = epi.prefetch(pm, col[j] + (threadIdx.x & 15));
     }
   }
+  // a second stage's own operands (EpiLinearConvGates), ahead of the stream
+  [[maybe_unused]] auto post_pf = [&] {
+    if constexpr (EpiPost<Epi>::value) return epi.pre(M);
+    else return 0;
+  }();
   const int koff = 8 * (lane >> 4);
   const int kbeg = blockIdx.y * klen;
   const int kend = min(K, kbeg + klen);
@@ -1705,6 +1933,9 @@ __global__ __launch_bounds__(512) void gemm_stream_kernel(
       for (int j = 0; j < NREP; ++j) epi.apply(m, col[j] + c, v[j], g);
     }
   }
+  // a second stage in the same workgroups (EpiLinearConvGates: the RG-LRU
+  // gate item), reusing the reduction buffer
+  if constexpr (EpiPost<Epi>::value) epi.post(&red[0][0], M, post_pf);
 }
 
 // Decode residual projection of one K split (1..32 packed rows in MR = 1 or 2 16-row tiles,
@@ -3087,7 +3318,7 @@ __attribute__((visibility("hidden"))) int cadence_engine_bits() { return g_engin
 
 extern "C" {
 
-int cadence_abi_version(void) { return 17; }
+int cadence_abi_version(void) { return 18; }
 
 int cadence_gemm_set_engine(int engine) {
   const int prev = g_engine;
@@ -3183,6 +3414,68 @@ int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
     case 3: run(std::integral_constant<int, 3>{}); break;
     default: run(std::integral_constant<int, 4>{}); break;
   }
+  return (int)hipGetLastError();
+}
+
+int cadence_recurrent_decode_front_plan(int64_t M, int64_t E, int64_t K, int64_t heads,
+                                        int64_t bw) {
+  int ksw = 0, ss = 0;
+  // the one instantiation the gate stage is written for: packed rows of 17..32
+  // sequences, 32 y|x columns per workgroup (ten 32-deep k-steps per wave, one
+  // K split), 2 bw / 32 workgroups per head = the head's gate items, the
+  // whole grid resident at once (<= 256 workgroups: one round).  (Two column
+  // tiles per workgroup whatever stream_ntw picks for the plain launch: a
+  // column's k-steps, waves and reduction order do not depend on NTW.)
+  return (M > 16 && M <= 32 && bw > 0 && bw % 64 == 0 && bw <= 256 && heads * bw == E &&
+          K % 32 == 0 && stream_plan(M, K, &ksw, &ss) && ksw == 10 && ss == 1 &&
+          2 * E / 32 <= 256) ? 1 : 0;
+}
+
+int cadence_recurrent_decode_front(const void* A, const void* Wyx, const void* bias,
+                                   void* yx_out, int64_t M, int64_t E, int64_t K,
+                                   const void* conv_w, const void* conv_b, void* conv_state,
+                                   int norm, float norm_eps, const void* Wgates,
+                                   const void* bias_x, const void* bias_a,
+                                   const void* softplus_a, const int32_t* segment_pos,
+                                   float* h, void* y_out, int64_t heads, int64_t bw,
+                                   int32_t* counters, int32_t* err, void* stream) {
+  if (M <= 0) return 0;
+  const int64_t N = 2 * E;
+  if (!cadence_recurrent_decode_front_plan(M, E, K, heads, bw) || !Wyx || !Wgates ||
+      !conv_w || !conv_b || !conv_state || !h || !y_out || !yx_out || !counters || !err ||
+      !segment_pos)
+    return (int)hipErrorInvalidValue;
+  EpiLinearConvGates<4> epi{};
+  static_cast<EpiLinear&>(epi) = EpiLinear{static_cast<u16*>(yx_out), N,
+                                           static_cast<const u16*>(bias), nullptr, 0, 0,
+                                           RowMap{M, 0, 0}, 0.0f};
+  epi.cw = static_cast<const u16*>(conv_w);
+  epi.cb = static_cast<const u16*>(conv_b);
+  epi.state = static_cast<u16*>(conv_state);
+  epi.conv_lo = (int)E;
+  epi.E = (int)E;
+  u16* yx = static_cast<u16*>(yx_out);
+  epi.ge = EpiRglruGates{yx + E, N, static_cast<const u16*>(bias_x),
+                         static_cast<const u16*>(bias_a), static_cast<const u16*>(softplus_a),
+                         segment_pos, nullptr, nullptr, 0, (int)bw, h, E, yx, N,
+                         static_cast<u16*>(y_out), 0, (int)((M + 15) / 16)};
+  epi.wg = static_cast<const u16*>(Wgates);
+  epi.cnt = counters;
+  epi.err = err;
+  const int klen = (int)K;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (norm)
+    hipLaunchKernelGGL((gemm_stream_kernel<32, 10, 2, EpiLinearConvGates<4>, true>),
+                       dim3((unsigned)(N / 32), 1, 1), dim3(512), 0, st,
+                       static_cast<const u16*>(A), (int64_t)0, static_cast<const u16*>(Wyx),
+                       (int64_t)0, (int)M, (int)N, (int)K, klen, (int64_t)0, (int64_t)0,
+                       nullptr, epi, 1, nullptr, norm_eps);
+  else
+    hipLaunchKernelGGL((gemm_stream_kernel<32, 10, 2, EpiLinearConvGates<4>, false>),
+                       dim3((unsigned)(N / 32), 1, 1), dim3(512), 0, st,
+                       static_cast<const u16*>(A), (int64_t)0, static_cast<const u16*>(Wyx),
+                       (int64_t)0, (int)M, (int)N, (int)K, klen, (int64_t)0, (int64_t)0,
+                       nullptr, epi, 1, nullptr, 0.0f);
   return (int)hipGetLastError();
 }
 

@@ -142,6 +142,30 @@ int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
                                int64_t temporal_width, int norm,
                                float norm_eps, void* stream);
 
+/* Decode recurrent-block front in ONE launch: cadence_gemm_linear_conv1d
+ * (conv_lo = E, TW = 4, packed W and A) followed, in the same workgroups, by
+ * cadence_rglru_step on its output with gate = the y branch and packed-rows
+ * y_out (reference modules.py:340-352 linear_y / linear_x, layers.py:478-483
+ * the Conv1D step, layers.py:345-365 + :175-182 the RG-LRU gates and T == 1
+ * scan step).  yx_out [M][2E] row-major receives (y, conv1d(x)) as
+ * cadence_gemm_linear_conv1d writes them; conv_state and h advance in place;
+ * y_out (packed rows) = bf16(h) * y.  Wgates: the decode-packed [heads][2 bw][bw]
+ * gate weights of cadence_rglru_step.  Bitwise equal to the two launches.
+ * Each head's 2 bw / 32 workgroups wait for one another (one agent-scope
+ * counter per head): counters = >= 2 * heads zeroed int32, left zeroed;
+ * err (int32) is set to 1 if a wait gave up (never expected).  Accepted
+ * shapes: cadence_recurrent_decode_front_plan. */
+int cadence_recurrent_decode_front_plan(int64_t M, int64_t E, int64_t K, int64_t heads,
+                                        int64_t bw);
+int cadence_recurrent_decode_front(const void* A, const void* Wyx, const void* bias,
+                                   void* yx_out, int64_t M, int64_t E, int64_t K,
+                                   const void* conv_w, const void* conv_b, void* conv_state,
+                                   int norm, float norm_eps, const void* Wgates,
+                                   const void* bias_x, const void* bias_a,
+                                   const void* softplus_a, const int32_t* segment_pos,
+                                   float* h, void* y_out, int64_t heads, int64_t bw,
+                                   int32_t* counters, int32_t* err, void* stream);
+
 /* Residual GEMM that feeds an RMSNorm (the temporal-block output projection
  * and ffw_down, each followed by the next norm; modules.py:908-913):
  *   out = A . W^T + bias + resid          (as cadence_gemm_linear, act 0)
