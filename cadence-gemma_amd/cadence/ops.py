@@ -485,7 +485,7 @@ def _recurrent_decode_front(a, a_rows, w, bias, conv_w, conv_b, conv_state, wg, 
   _need(h.dtype == _F32 and h.is_contiguous() and tuple(h.shape) == (M, E),
         "h: [M, E] fp32 contiguous")
   _need(segment_pos.dtype == _I32 and segment_pos.numel() == M, "segment_pos")
-  _need(counters.dtype == _I32 and counters.numel() >= 2 * H and
+  _need(counters.dtype == _I32 and counters.numel() >= 64 * H and
         err.dtype == _I32 and err.numel() >= 1, "counters / err")
   if bias is not None:
     _need(bias.numel() == N and bias.dtype == _BF16, "bias shape/dtype")
@@ -1384,7 +1384,7 @@ def recurrent_decode_front_(x2d, w, bias, conv_w, conv_b, conv_state, gates, pos
   a, ar, wd, nm = _an(x2d, w)
   if wd is None:
     return None
-  cnt, err = _counters(x2d.device, 2 * H), wait_err(x2d.device)
+  cnt, err = _counters(x2d.device, 64 * H), wait_err(x2d.device)
   if cnt is None or err is None:
     return None
   _, y = ops.recurrent_decode_front(a, ar, wd, bias, conv_w, conv_b, conv_state, wg, bx, ba,

@@ -678,8 +678,14 @@ struct EpiRglruGates {
 // round, so the awaited workgroups are running or about to be).  The gate
 // weights and the epilogue's other operands are loaded before the wait.
 // Same fragments, k order, reduction order and epilogue as the two
-// launches: bitwise equal (tests/test_recurrent_front_gpu.py).  Counters:
-// cnt[head] counts arrivals, cnt[heads + head] departures; the head's last
+// launches: bitwise equal (tests/test_recurrent_front_gpu.py).  Measured
+// SLOWER than the two launches in the graph-replayed decode (15.3 us against
+// 9.1 + 5.0, +21..54 us per token: profiles/r06t_front/): the hand-off chain
+// after the last y|x workgroup of a head -- drain 0.5 us, arrival seen 1.2,
+// cross-XCD x reload + MFMA 1.1, epilogue 0.55 -- costs what the launch
+// boundary and the gate kernel's own ramp cost.  Off by default
+// (ops.FRONT_ONE_LAUNCH).  Counters:
+// cnt[32 head] counts arrivals, cnt[32 (heads + head)] departures; the head's last
 // workgroup to depart zeroes both (every workgroup departs only after its
 // own wait saw all arrivals), so the buffer is left as it was found.
 template <class E, class = void>
@@ -706,7 +712,11 @@ struct EpiLinearConvGates : EpiLinearConv<TW> {
   static constexpr bool kPost = true;
   EpiRglruGates ge;     // x = out + conv_lo (ldx = ldo), gate = out (ldg = ldo), packed y
   const u16* wg;        // decode-packed gate weights [H][2 bw / 16][bw / 32][64][8]
-  int32_t* cnt;         // [2 H] arrive / depart counters, zero before and after
+  // [2 H] arrive / depart counters, zero before and after, one per 128-B
+  // line (polled by every workgroup of the head: one shared line for all
+  // heads put the arrivals 4-5 us behind: profiles/r06t_front/)
+  static constexpr int kCntStride = 32;
+  int32_t* cnt;
   int32_t* err;         // set to 1 if an arrival wait gave up (never expected)
   using Pref = typename EpiLinearConv<TW>::Pref;
   // this workgroup's [32 rows][32 columns] of `out`, staged so that the
@@ -806,7 +816,7 @@ struct EpiLinearConvGates : EpiLinearConv<TW> {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0)
-      __hip_atomic_fetch_add(cnt + head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(cnt + kCntStride * head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int K = bw;
     const int k = wave * 32, koff = 8 * (lane >> 4);
     const bool ok = k < K;
@@ -818,7 +828,7 @@ struct EpiLinearConvGates : EpiLinearConv<TW> {
     // 3. every workgroup of the head has published
     if (tid == 0) {
       int n = 0;
-      while (__hip_atomic_load(cnt + head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < per) {
+      while (__hip_atomic_load(cnt + kCntStride * head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < per) {
         __builtin_amdgcn_s_sleep(1);
         if (++n == (1 << 24)) {   // give up rather than hang the queue (never expected)
           __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -875,11 +885,11 @@ struct EpiLinearConvGates : EpiLinearConv<TW> {
     }
     // 6. depart; the head's last workgroup to depart zeroes both counters
     if (tid == 0) {
-      const int d = __hip_atomic_fetch_add(cnt + heads + head, 1, __ATOMIC_RELAXED,
+      const int d = __hip_atomic_fetch_add(cnt + kCntStride * (heads + head), 1, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
       if (d == per - 1) {
-        __hip_atomic_store(cnt + head, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(cnt + heads + head, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt + kCntStride * head, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt + kCntStride * (heads + head), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }

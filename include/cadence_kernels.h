@@ -152,7 +152,8 @@ int cadence_gemm_linear_conv1d(const void* A, int64_t lda, const void* W,
  * y_out (packed rows) = bf16(h) * y.  Wgates: the decode-packed [heads][2 bw][bw]
  * gate weights of cadence_rglru_step.  Bitwise equal to the two launches.
  * Each head's 2 bw / 32 workgroups wait for one another (one agent-scope
- * counter per head): counters = >= 2 * heads zeroed int32, left zeroed;
+ * counter per head, one per 128-B line): counters = >= 64 * heads zeroed
+ * int32, left zeroed;
  * err (int32) is set to 1 if a wait gave up (never expected).  Accepted
  * shapes: cadence_recurrent_decode_front_plan. */
 int cadence_recurrent_decode_front_plan(int64_t M, int64_t E, int64_t K, int64_t heads,

@@ -38,6 +38,11 @@ def _case(dev, m, e, heads, k, gen):
   return w, bias, cw, cb, state, (wg, bx, ba, sp), pos.to(dev), h
 
 
+@pytest.fixture(autouse=True)
+def _one_launch(monkeypatch):
+  monkeypatch.setattr(ops, "FRONT_ONE_LAUNCH", True)
+
+
 def _rows(dev, m, k, gen, norm):
   x = rnd(m, k, gen=gen).to(dev)
   if not norm:
@@ -76,8 +81,8 @@ def test_recurrent_front_matches_two_launches(dev, m, e, heads, k, norm):
     assert torch.equal(y_got.unpack(), y_ref.unpack()), it
     assert torch.equal(s_got, s_ref), it
     assert torch.equal(h_got, h_ref), it
-    cnt = ops._counters(dev, 2 * heads)
-    assert int(cnt[:2 * heads].abs().sum()) == 0, it
+    cnt = ops._counters(dev, 64 * heads)
+    assert int(cnt[:64 * heads].abs().sum()) == 0, it
     assert int(err) == 0
   # the (y, conv1d(x)) output of the same launch
   a, ar, wd, nm = ops._an(x, w)
@@ -85,7 +90,7 @@ def test_recurrent_front_matches_two_launches(dev, m, e, heads, k, norm):
   h3 = h.clone()
   wg = ops.decode_weight(gates[0])
   yx, _ = ops.ops.recurrent_decode_front(a, ar, wd, bias, cw, cb, s3, wg, *gates[1:], pos, h3,
-                                         ops._counters(dev, 2 * heads), err, nm is not None,
+                                         ops._counters(dev, 64 * heads), err, nm is not None,
                                          float(nm.eps) if nm is not None else 0.0)
   want = ops.linear_conv1d_(x, w, bias, cw, cb, state.clone())
   assert torch.equal(yx, want)
