@@ -74,7 +74,8 @@ def evaluate(name, seed):
 
 
 def main():
-  torch.set_num_threads(min(8, os.cpu_count() or 1))
+  torch.set_num_threads(int(os.environ.get("SEED_SEARCH_THREADS", 0)) or
+                        min(8, os.cpu_count() or 1))
   name, need, lead_need = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
   for seed in [int(s) for s in sys.argv[4:]]:
     t0 = time.time()
