@@ -55,7 +55,7 @@ N_FEATURE_ROWS = 24
 # the only size the reference itself accepts (griffin.py:186-191).
 CONFIGS = {
     "c1": (None, 1, 16, 8, 101),
-    "c2": (None, 1, 2048, 8, 115),
+    "c2": (None, 1, 2048, 8, 132),
     "c3": (224, 1, 64, 8, 203),
     "bench224": (224, 2, 64, 8, 287),
     "c4": (336, 1, 64, 8, 313),
