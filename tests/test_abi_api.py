@@ -8,7 +8,7 @@ import pytest
 import torch
 
 import cadence
-from cadence import _lib, common
+from cadence import _lib, common, ops
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "cadence_kernels.h")
@@ -277,3 +277,24 @@ def test_vit_attention_plan_query():
     assert (plan(256, 72), plan(581, 64)) == (0, 1)
   finally:
     lib.cadence_gemm_set_engine(prev)
+
+
+def test_recurrent_decode_front_plan_query():
+  """cadence_recurrent_decode_front_plan (host-only): the one-launch decode
+  recurrent front takes 17..32 rows, gate blocks of 64..256 channels that
+  tile the width, and a K that the weight-streaming engine covers in one
+  split of ten 32-deep k-steps per wave; the host mirror leaves it off by
+  default (measured slower than the two launches)."""
+  lib = _lib.load()
+  plan = lib.cadence_recurrent_decode_front_plan
+  assert plan(32, 2560, 2560, 10, 256) == 1            # CadenceGemma-2B, bench batch
+  assert plan(17, 2560, 2560, 10, 256) == 1
+  assert plan(24, 1024, 1280, 8, 128) == 1
+  assert plan(16, 2560, 2560, 10, 256) == 0            # one 16-row tile
+  assert plan(33, 2560, 2560, 10, 256) == 0            # not decode rows
+  assert plan(32, 2560, 2560, 10, 192) == 0            # block width
+  assert plan(32, 2560, 2560, 9, 256) == 0             # heads x bw != E
+  assert plan(32, 2560, 1024, 10, 256) == 0            # K below the 10-step plan
+  assert plan(32, 2560, 7680, 10, 256) == 0            # K needs a split
+  assert plan(32, 5120, 2560, 20, 256) == 0            # > 256 workgroups
+  assert ops.FRONT_ONE_LAUNCH is False
