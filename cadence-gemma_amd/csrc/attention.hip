@@ -562,14 +562,16 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
     // first use; ranges past 8 (only B <= 16) take another trip per 8.
     constexpr int GS = 8, QP = HD / 64;   // QP x 256 float4 >= 16 heads x HD
     const int nq = a.H * HD / 4;
-    float mx[QP], l[QP];
+    // the running rescale's factors depend on (head row, range) only: one
+    // lane per head row walks the ranges once (the same operations in the
+    // same order as a per-element walk, so the same bits) and every thread
+    // applies them -- per-thread, the walk cost 2 expf per (chunk, range),
+    // 3.5-5 us of the combine at B = 32 (profiles/r06v_decode_attn_phases/)
+    __shared__ float2 fac[kDecodeSplitsMax * 16];   // (scale of the sum so far, of range u)
+    __shared__ float lfin[16];
     f32x4 acc[QP];
 #pragma unroll
-    for (int p = 0; p < QP; ++p) {
-      mx[p] = -INFINITY;
-      l[p] = 0.0f;
-      acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int p = 0; p < QP; ++p) acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int idx = tid; idx < nsp * 32; idx += 256)
       mls[idx] = __hip_atomic_load(pb + (idx >> 5) * PS + (idx & 31), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -586,21 +588,32 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
         }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();   // the (m, l) rows are in LDS
+      if (s0 == 0) {
+        if (tid < 16) {
+          // running rescale in range order, head row tid
+          float mx = -INFINITY, l = 0.0f;
+          for (int u = 0; u < nsp; ++u) {
+            const float mu = mls[u * 32 + tid], lu = mls[u * 32 + 16 + tid];
+            const float mn = fmaxf(mx, mu);
+            const float sa = mx == -INFINITY ? 0.0f : expf(mx - mn);
+            const float sb = mu == -INFINITY ? 0.0f : expf(mu - mn);
+            l = l * sa + lu * sb;
+            fac[u * 16 + tid] = make_float2(sa, sb);
+            mx = mn;
+          }
+          lfin[tid] = l;
+        }
+        __syncthreads();
+      }
 #pragma unroll
       for (int p = 0; p < QP; ++p) {
         const int hrow = min(tid + 256 * p, nq - 1) * 4 / HD;
 #pragma unroll
         for (int u = 0; u < GS; ++u) {
           if (s0 + u >= nsp) continue;
-          // running rescale in range order
-          const float mu = mls[(s0 + u) * 32 + hrow], lu = mls[(s0 + u) * 32 + 16 + hrow];
-          const float mn = fmaxf(mx[p], mu);
-          const float sa = mx[p] == -INFINITY ? 0.0f : expf(mx[p] - mn);
-          const float sb = mu == -INFINITY ? 0.0f : expf(mu - mn);
-          l[p] = l[p] * sa + lu * sb;
+          const float2 f = fac[(s0 + u) * 16 + hrow];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[p][e] = acc[p][e] * sa + w[p][u][e] * sb;
-          mx[p] = mn;
+          for (int e = 0; e < 4; ++e) acc[p][e] = acc[p][e] * f.x + w[p][u][e] * f.y;
         }
       }
     }
@@ -608,7 +621,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
     for (int p = 0; p < QP; ++p) {
       const int c = tid + 256 * p;
       if (c >= nq) continue;
-      const float inv = l[p] > 0.0f ? 1.0f / l[p] : 0.0f;
+      const float lp = lfin[c * 4 / HD];
+      const float inv = lp > 0.0f ? 1.0f / lp : 0.0f;
       u16* dst = a.o + xoff(b, 4 * c, a.ldo, a.omt);
       const uint32_t lo = (uint32_t)f2bf(acc[p][0] * inv) | ((uint32_t)f2bf(acc[p][1] * inv) << 16);
       const uint32_t hi = (uint32_t)f2bf(acc[p][2] * inv) | ((uint32_t)f2bf(acc[p][3] * inv) << 16);
