@@ -333,6 +333,30 @@ CADENCE_DEV int vswz(int row) {
   return CPR >= 16 ? 2 * ((row & 3) | (((row >> 3) & 1) << 2)) : 2 * (row & 3);
 }
 
+// Reductions over the 16 lanes of a DPP row (the 16 key columns of a score
+// block) on the VALU's DPP lane moves -- quad xor 1, quad xor 2, half-row
+// mirror, row mirror -- instead of four ds_bpermute round trips through the
+// LDS pipe.  After the two quad steps every lane of a quad holds bitwise the
+// same value (IEEE max / add are commutative), so pairing lane i with 7 - i
+// and then 15 - i combines the same operands as xor 4 and xor 8: the same
+// bits as the __shfl_xor butterfly.
+template <int CTRL>
+CADENCE_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+CADENCE_DEV float row16_max(float t) {
+  t = fmaxf(t, dpp_f<0xb1>(t));    // quad_perm [1, 0, 3, 2]
+  t = fmaxf(t, dpp_f<0x4e>(t));    // quad_perm [2, 3, 0, 1]
+  t = fmaxf(t, dpp_f<0x141>(t));   // row_half_mirror
+  return fmaxf(t, dpp_f<0x140>(t));  // row_mirror
+}
+CADENCE_DEV float row16_sum(float t) {
+  t += dpp_f<0xb1>(t);
+  t += dpp_f<0x4e>(t);
+  t += dpp_f<0x141>(t);
+  return t + dpp_f<0x140>(t);
+}
+
 template <int HD>
 __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
   constexpr int KS = HD / 32, NO = HD / 64, CPR = HD / 8;
@@ -457,8 +481,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float t = tmax[r];
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) t = fmaxf(t, __shfl_xor(t, off, 64));
+      t = row16_max(t);
       const float mn = fmaxf(m_run[r], t);
       alpha[r] = (mn == -INFINITY) ? 1.0f : expf(m_run[r] - mn);
       float rs = 0.0f;
@@ -468,8 +491,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
         p[jn][r] = e;
         rs += e;
       }
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off, 64);
+      rs = row16_sum(rs);
       l_run[r] = l_run[r] * alpha[r] + rs;
       m_run[r] = mn;
     }
